@@ -1,0 +1,165 @@
+/*
+ * slgpu.h — C ABI of the MI355X (gfx950) structured-light reconstruction library.
+ *
+ * Drop-in boundary for the hot path of TtT609/Structured_Light_for_3D_Model_Replication.
+ * The reference has no FFI: its boundary is the Python call surface, so each export below
+ * replaces one reference function (cited), and the Python package
+ * `structured_light_for_3d_model_replication_amd` binds these symbols with ctypes and keeps
+ * the reference's signatures.
+ *
+ *   slg_decode_stats       <- mask thresholds of ProcessingLogic._gray_decode
+ *                             (server/processing.py:59-78; Otsu / manual) and of
+ *                             SLSystem.generate_cloud.gray_decode (server/sl_system.py:527-543;
+ *                             95th-percentile / dynamic range)
+ *   slg_decode             <- ProcessingLogic._gray_decode (server/processing.py:28-124) and
+ *                             generate_cloud.gray_decode (server/sl_system.py:516-588)
+ *   slg_triangulate        <- ProcessingLogic._reconstruct_point_cloud
+ *                             (server/processing.py:127-234) and
+ *                             generate_cloud.reconstruct_point_cloud (server/sl_system.py:592-661)
+ *   slg_reconstruct        <- decode + triangulate of one view as run by
+ *                             process_multi_ply._process_source (server/processing.py:286-298)
+ *                             without materialising the correspondence maps
+ *   slg_rays_match_pinhole <- the `Nc.shape[1] == h*w` ray source test
+ *                             (server/processing.py:143-156): tells whether the calibration's
+ *                             Nc table equals the cam_K pinhole rays bit for bit, in which case
+ *                             the kernels recompute rays instead of gathering 24 B/pixel.
+ *
+ * Conventions
+ *   - All buffer pointers are DEVICE pointers owned by the caller (the library never
+ *     allocates or frees caller memory); scratch lives in a caller-provided workspace of
+ *     slg_workspace_bytes() bytes, zeroed once with slg_workspace_init().
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  Every export only
+ *     enqueues work (no host synchronisation), so calls can be captured into a hipGraph.
+ *   - Return value: SLG_OK (0) or an SLG_ERR_* code; slg_last_error() returns a thread-local
+ *     message for the last failing call on the calling thread.
+ *   - Frames: uint8 [n_frames][frame_stride] planar stack in capture order (index 0 white,
+ *     1 black, then (pattern, inverse) per column bit MSB-first, then per row bit starting
+ *     at 2 + 2*ceil(log2(proj_cols))).  frame_stride % 8 == 0, base 8-byte aligned.
+ *   - Points are written in ascending pixel order (np.where(mask) order); row_mode 2 writes
+ *     the column cloud then the row cloud, like np.hstack((P_col, P_row)).
+ */
+#ifndef SLGPU_H
+#define SLGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SLG_ABI_VERSION 1
+
+#define SLG_OK 0
+#define SLG_ERR_INVALID 1      /* bad argument (message in slg_last_error) */
+#define SLG_ERR_HIP 2          /* HIP runtime / launch error */
+#define SLG_ERR_UNSUPPORTED 3  /* e.g. more than 15 code bits per axis */
+#define SLG_ERR_NOT_ENOUGH 4   /* fewer than 4 frames (reference: ValueError) */
+#define SLG_ERR_INDEX 5        /* odd trailing frame in the sl_system variant (IndexError) */
+
+/* thresh_mode */
+#define SLG_THRESH_OTSU 0        /* processing.py:63-72 */
+#define SLG_THRESH_MANUAL 1      /* processing.py:73-76 */
+#define SLG_THRESH_PERCENTILE 2  /* sl_system.py:534-540 */
+
+/* variant */
+#define SLG_VARIANT_PROCESSING 0 /* ProcessingLogic._gray_decode: first-n bits, rescaled */
+#define SLG_VARIANT_SLSYSTEM 1   /* generate_cloud.gray_decode: all bits, break on missing */
+
+/* ray_mode */
+#define SLG_RAYS_TABLE 0         /* gather Nc[:, idx] (processing.py:143-144) */
+#define SLG_RAYS_PINHOLE 1       /* recompute from cam_K (processing.py:145-156) */
+
+typedef struct slg_capture {
+  const uint8_t *frames;   /* device, [n_frames][frame_stride] */
+  int64_t frame_stride;    /* bytes between frames (>= height*width, % 8 == 0) */
+  int32_t n_frames;        /* frames present (len(files)) */
+  int32_t height;
+  int32_t width;
+  int32_t reserved;
+  const uint8_t *texture;  /* device, [height*width][3] BGR (cv2.imread(files[0])) */
+} slg_capture;
+
+typedef struct slg_decode_params {
+  int32_t proj_cols;       /* n_cols  (processing.py:28) */
+  int32_t proj_rows;       /* n_rows */
+  int32_t n_sets_col;      /* processing variant only (processing.py:83) */
+  int32_t n_sets_row;
+  int32_t variant;         /* SLG_VARIANT_* */
+  int32_t thresh_mode;     /* SLG_THRESH_* */
+  double shadow_val;       /* manual: compared as double; pass float32-rounded values for */
+  double contrast_val;     /* NumPy-2 weak-scalar semantics (the Python layer does this) */
+} slg_decode_params;
+
+typedef struct slg_calib {
+  const double *rays;      /* device (3, height*width) C-contiguous, or NULL (SLG_RAYS_PINHOLE) */
+  int32_t ray_mode;        /* SLG_RAYS_* */
+  int32_t reserved;
+  double fx, fy, cx, cy;   /* cam_K[0,0], cam_K[1,1], cam_K[0,2], cam_K[1,2] */
+  double oc[3];            /* Oc (always 0 from calibrate_final, sl_system.py:355) */
+  const double *col_planes;/* device (n_col_planes, 4) row-major = wPlaneCol.T */
+  int32_t n_col_planes;
+  int32_t reserved2;
+  const double *row_planes;/* device (n_row_planes, 4) row-major = wPlaneRow.T */
+  int32_t n_row_planes;
+  int32_t reserved3;
+} slg_calib;
+
+typedef struct slg_tri_params {
+  int32_t row_mode;        /* 0 col only, 1 epipolar filter, 2 col+row clouds (processing.py:174-234) */
+  int32_t xyz_f64;         /* 1: XYZ float64 (bit-exact with the reference); 0: float32 */
+  double epipolar_tol;     /* processing.py:199 */
+} slg_tri_params;
+
+typedef struct slg_maps {
+  const int32_t *col;      /* device [height*width] */
+  const int32_t *row;      /* device [height*width] (may be NULL for row_mode 0) */
+  const uint8_t *mask;     /* device [height*width] bool */
+  const uint8_t *texture;  /* device [height*width][3] BGR */
+  int32_t height;
+  int32_t width;
+} slg_maps;
+
+typedef struct slg_cloud {
+  void *xyz;               /* device [capacity][3] float or double */
+  uint8_t *bgr;            /* device [capacity][3] */
+  int64_t *count;          /* device, 1 element: number of points written */
+  int64_t capacity;        /* >= height*width (row_mode 0/1) or 2*height*width (row_mode 2) */
+} slg_cloud;
+
+int32_t slg_version(void);
+const char *slg_last_error(void);
+
+/* Workspace size for images of n_pixels (covers every mode). */
+int64_t slg_workspace_bytes(int64_t n_pixels);
+/* Zero a freshly allocated workspace (once; the kernels keep it consistent afterwards). */
+int32_t slg_workspace_init(void *workspace, int64_t workspace_bytes, void *stream);
+
+/* Histograms + thresholds of the valid mask into the workspace; also arms the workspace for
+ * the next slg_decode / slg_reconstruct on the same stream. */
+int32_t slg_decode_stats(const slg_capture *cap, const slg_decode_params *dp, void *workspace,
+                         void *stream);
+
+/* Gray decode to correspondence maps (after slg_decode_stats on the same workspace). */
+int32_t slg_decode(const slg_capture *cap, const slg_decode_params *dp, void *workspace,
+                   int32_t *col_out, int32_t *row_out, uint8_t *mask_out, void *stream);
+
+/* Ray-plane triangulation + ordered compaction from maps.  Arms the workspace itself. */
+int32_t slg_triangulate(const slg_maps *maps, const slg_calib *calib, const slg_tri_params *tp,
+                        void *workspace, const slg_cloud *out, void *stream);
+
+/* Fused: stats + decode + triangulate + compaction of one view (maps never hit HBM). */
+int32_t slg_reconstruct(const slg_capture *cap, const slg_decode_params *dp,
+                        const slg_calib *calib, const slg_tri_params *tp, void *workspace,
+                        const slg_cloud *out, void *stream);
+
+/* Count (into *mismatches, device int64) the Nc entries that differ bitwise from the cam_K
+ * pinhole rays; 0 means SLG_RAYS_PINHOLE reproduces the table exactly. */
+int32_t slg_rays_match_pinhole(const double *rays, int32_t height, int32_t width, double fx,
+                               double fy, double cx, double cy, int64_t *mismatches,
+                               void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SLGPU_H */

@@ -1,0 +1,126 @@
+"""ctypes binding of ``libslgpu.so`` (C ABI in ``include/slgpu.h``).
+
+The library is built in-tree (``build.build_native``) and must be present: there is no CPU
+fallback in the product path.  ``torch`` is imported first so that the library's
+``libamdhip64.so.7`` dependency resolves to the HIP runtime torch already loaded (one HIP
+runtime per process; a second one would not understand torch's streams or pointers).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_NAME = "libslgpu.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+SLG_OK = 0
+SLG_ERR_INVALID = 1
+SLG_ERR_HIP = 2
+SLG_ERR_UNSUPPORTED = 3
+SLG_ERR_NOT_ENOUGH = 4
+SLG_ERR_INDEX = 5
+
+THRESH_OTSU, THRESH_MANUAL, THRESH_PERCENTILE = 0, 1, 2
+VARIANT_PROCESSING, VARIANT_SLSYSTEM = 0, 1
+RAYS_TABLE, RAYS_PINHOLE = 0, 1
+
+c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+
+
+class Capture(ctypes.Structure):
+    _fields_ = [("frames", c_vp), ("frame_stride", c_i64), ("n_frames", c_i32),
+                ("height", c_i32), ("width", c_i32), ("reserved", c_i32), ("texture", c_vp)]
+
+
+class DecodeParams(ctypes.Structure):
+    _fields_ = [("proj_cols", c_i32), ("proj_rows", c_i32), ("n_sets_col", c_i32),
+                ("n_sets_row", c_i32), ("variant", c_i32), ("thresh_mode", c_i32),
+                ("shadow_val", c_dbl), ("contrast_val", c_dbl)]
+
+
+class Calib(ctypes.Structure):
+    _fields_ = [("rays", c_vp), ("ray_mode", c_i32), ("reserved", c_i32),
+                ("fx", c_dbl), ("fy", c_dbl), ("cx", c_dbl), ("cy", c_dbl),
+                ("oc", c_dbl * 3), ("col_planes", c_vp), ("n_col_planes", c_i32),
+                ("reserved2", c_i32), ("row_planes", c_vp), ("n_row_planes", c_i32),
+                ("reserved3", c_i32)]
+
+
+class TriParams(ctypes.Structure):
+    _fields_ = [("row_mode", c_i32), ("xyz_f64", c_i32), ("epipolar_tol", c_dbl)]
+
+
+class Maps(ctypes.Structure):
+    _fields_ = [("col", c_vp), ("row", c_vp), ("mask", c_vp), ("texture", c_vp),
+                ("height", c_i32), ("width", c_i32)]
+
+
+class Cloud(ctypes.Structure):
+    _fields_ = [("xyz", c_vp), ("bgr", c_vp), ("count", c_vp), ("capacity", c_i64)]
+
+
+EXPORTS = {
+    "slg_version": (c_i32, []),
+    "slg_last_error": (ctypes.c_char_p, []),
+    "slg_workspace_bytes": (c_i64, [c_i64]),
+    "slg_workspace_init": (c_i32, [c_vp, c_i64, c_vp]),
+    "slg_decode_stats": (c_i32, [ctypes.POINTER(Capture), ctypes.POINTER(DecodeParams), c_vp, c_vp]),
+    "slg_decode": (c_i32, [ctypes.POINTER(Capture), ctypes.POINTER(DecodeParams), c_vp,
+                           c_vp, c_vp, c_vp, c_vp]),
+    "slg_triangulate": (c_i32, [ctypes.POINTER(Maps), ctypes.POINTER(Calib),
+                                ctypes.POINTER(TriParams), c_vp, ctypes.POINTER(Cloud), c_vp]),
+    "slg_reconstruct": (c_i32, [ctypes.POINTER(Capture), ctypes.POINTER(DecodeParams),
+                                ctypes.POINTER(Calib), ctypes.POINTER(TriParams), c_vp,
+                                ctypes.POINTER(Cloud), c_vp]),
+    "slg_rays_match_pinhole": (c_i32, [c_vp, c_i32, c_i32, c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_vp]),
+}
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"slgpu error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the native library; raises if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; "
+                              f"g.build()'` (hipcc --offload-arch=gfx950) first")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        if h.slg_version() != 1:
+            raise ImportError("libslgpu ABI version mismatch")
+        _lib = h
+    return _lib
+
+
+def check(rc: int):
+    if rc != SLG_OK:
+        msg = lib().slg_last_error().decode(errors="replace")
+        if rc == SLG_ERR_NOT_ENOUGH:
+            raise ValueError(msg)
+        if rc == SLG_ERR_INDEX:
+            raise IndexError(msg)
+        raise NativeError(rc, msg)
+
+
+def loaded_hip_runtimes() -> list[str]:
+    """Paths of every libamdhip64 mapped into this process (must be exactly one)."""
+    out = set()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64" in line:
+                out.add(line.split()[-1])
+    return sorted(out)

@@ -1,0 +1,37 @@
+"""In-tree build of the native library (hipcc, gfx950).  No JIT cache: the ``.so`` lives next
+to the sources so that it travels with the repository snapshot to the GPU box."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+SRC = os.path.join(PKG, "csrc", "slgpu.hip")
+HDR = os.path.join(ROOT, "include", "slgpu.h")
+OUT = os.path.join(PKG, "libslgpu.so")
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared"]
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(p) > t for p in (SRC, HDR, __file__))
+
+
+def build_native(force: bool = False, verbose: bool = False) -> str:
+    """Compile ``csrc/slgpu.hip`` into ``libslgpu.so`` (skipped when up to date)."""
+    if force or needs_build():
+        cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", SRC]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build_native(force=True, verbose=True))

@@ -1,0 +1,973 @@
+// slgpu.hip — MI355X (gfx950, CDNA4) kernels for the structured-light hot path.
+//
+// Path (reference): Gray-code decode  server/processing.py:28-124, server/sl_system.py:516-588
+//                   ray-plane triangulation  server/processing.py:127-234, sl_system.py:592-661
+// C ABI: include/slgpu.h.  Design and rooflines: DESIGN.md.
+//
+// Kernels
+//   stats_kernel      white/black histograms (+ max contrast) -> last-arriving workgroup turns
+//                     them into integer mask thresholds (Otsu as OpenCV, or NumPy percentile);
+//                     also zeroes the compaction state of the next main launch.
+//   main_kernel<...>  one 2048-pixel tile per workgroup (256 lanes x 8 pixels): streams the
+//                     used frames with 8-byte-per-lane coalesced loads, SWAR byte compares,
+//                     packed 16-bit Gray->binary, optional map stores, fp64 ray-plane
+//                     intersection, ordered compaction (block scan + decoupled look-back over
+//                     dynamic tile ids) staged through LDS and written with coalesced stores.
+//   row_tail_kernel   row_mode 2: moves the row cloud behind the column cloud.
+//   pinhole_kernel    bitwise Nc == pinhole(cam_K) test.
+//
+// Numerics: every floating-point expression follows NumPy's operation order with
+// -ffp-contract=off (no FMA contraction), IEEE-correct f64 division and sqrt, so the fp64
+// results equal the reference bit for bit; integer/byte work is exact by construction.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+#include <string.h>
+#include <limits.h>
+#include <type_traits>
+
+#include "../../include/slgpu.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kBlock = 256;                 // 4 waves of 64
+constexpr int kPx = 8;                      // pixels per lane (one 8-byte load per frame)
+constexpr int kTilePx = kBlock * kPx;       // 2048 pixels per workgroup tile
+constexpr int kMaxBits = 15;                // packed 16-bit code lanes
+constexpr int kLookK = 16;                  // look-back window = 16 x 64 predecessor tiles
+constexpr uint64_t kFlagAgg = 1ull << 62;
+constexpr uint64_t kFlagInc = 2ull << 62;
+constexpr uint64_t kValMask = (1ull << 62) - 1;
+constexpr unsigned kMaxSpin = 1u << 22;
+
+// ------------------------------------------------------------------ workspace layout
+struct WsHeader {
+  uint32_t hist[3][256];   // 0: white, 1: clip(white-black,0,255), 2: black
+  uint32_t max_diff_enc;   // max(white-black) + 256 (0 = none yet)
+  uint32_t ticket;         // stats_kernel arrival counter
+  uint32_t tile_counter;   // dynamic tile id for main_kernel
+  uint32_t error;          // bit 0: look-back spin timeout
+  int32_t smin;            // mask: white >= smin
+  int32_t cmin;            //       (white - black) >= cmin
+  int32_t pad0[2];
+  double thr_s;            // float thresholds (for inspection / tests)
+  double thr_c;
+  int64_t totals[2];       // column / row stream point totals
+};
+constexpr int64_t kHeaderBytes = 8192;
+static_assert(sizeof(WsHeader) <= kHeaderBytes, "header");
+
+__host__ __device__ inline int64_t n_tiles_of(int64_t n_px) { return (n_px + kTilePx - 1) / kTilePx; }
+__host__ __device__ inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+__host__ __device__ inline int64_t states_off(int64_t) { return kHeaderBytes; }
+__host__ __device__ inline int64_t states_bytes(int64_t n_px) { return align_up(2 * n_tiles_of(n_px) * 8, 256); }
+__host__ __device__ inline int64_t scratch_xyz_off(int64_t n_px) { return kHeaderBytes + states_bytes(n_px); }
+__host__ __device__ inline int64_t scratch_bgr_off(int64_t n_px) { return scratch_xyz_off(n_px) + align_up(n_px * 24, 256); }
+__host__ __device__ inline int64_t ws_total(int64_t n_px) { return scratch_bgr_off(n_px) + align_up(n_px * 3, 256); }
+
+// ------------------------------------------------------------------ small helpers
+__device__ inline uint64_t ld_state(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_state(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class T>
+__device__ inline T wave_sum(T x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+__device__ inline int wave_min_i(int x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o));
+  return x;
+}
+
+// Per-byte unsigned p > i on 4 packed bytes: 0x80 in every byte lane where p > i.
+__device__ inline uint32_t gt_u8x4(uint32_t p, uint32_t i) {
+  const uint32_t d = (i | 0x80808080u) - (p & 0x7f7f7f7fu);   // hi bit: low7(i) >= low7(p)
+  return ((p & ~i) | (~(p ^ i) & ~d)) & 0x80808080u;
+}
+
+// Gray -> binary on two packed 16-bit lanes (values < 2^15): prefix XOR from the top.
+__device__ inline uint32_t gray2bin_x2(uint32_t x) {
+  x ^= (x >> 1) & 0x7fff7fffu;
+  x ^= (x >> 2) & 0x3fff3fffu;
+  x ^= (x >> 4) & 0x0fff0fffu;
+  x ^= (x >> 8) & 0x00ff00ffu;
+  return x;
+}
+
+// 8 bytes of a plane starting at pixel px0; tail-safe.
+__device__ inline uint2 load8(const uint8_t* base, int64_t px0, int64_t n_px) {
+  if (px0 + kPx <= n_px) return *reinterpret_cast<const uint2*>(base + px0);
+  uint32_t w[2] = {0u, 0u};
+  for (int k = 0; k < kPx; ++k)
+    if (px0 + k < n_px) w[k >> 2] |= uint32_t(base[px0 + k]) << (8 * (k & 3));
+  return make_uint2(w[0], w[1]);
+}
+
+// ------------------------------------------------------------------ stats kernel
+struct StatsParams {
+  const uint8_t* white;
+  const uint8_t* black;
+  int64_t n_px;
+  WsHeader* ws;
+  uint64_t* states;        // zeroed here for the next main launch
+  int64_t n_state_words;
+  int32_t thresh_mode;
+  int32_t pad;
+  double shadow_val;
+  double contrast_val;
+};
+
+// OpenCV getThreshVal_Otsu_8u, sequential fp64 (see oracle/sl_oracle.py:otsu_from_hist).
+__device__ double otsu_from_hist(const uint32_t* h, int64_t total) {
+  const double scale = 1.0 / double(total);
+  double mu = 0.0;
+  for (int i = 0; i < 256; ++i) mu += double(i) * double(h[i]);
+  mu *= scale;
+  double mu1 = 0.0, q1 = 0.0, max_sigma = 0.0, max_val = 0.0;
+  const double eps = double(__FLT_EPSILON__);
+  for (int i = 0; i < 256; ++i) {
+    const double p_i = double(h[i]) * scale;
+    mu1 *= q1;
+    q1 += p_i;
+    const double q2 = 1.0 - q1;
+    if (fmin(q1, q2) < eps || fmax(q1, q2) > 1.0 - eps) continue;
+    mu1 = (mu1 + double(i) * p_i) / q1;
+    const double mu2 = (mu - q1 * mu1) / q2;
+    const double sigma = q1 * q2 * (mu1 - mu2) * (mu1 - mu2);
+    if (sigma > max_sigma) {
+      max_sigma = sigma;
+      max_val = double(i);
+    }
+  }
+  return max_val;
+}
+
+// k-th smallest value (0-based) from a 256-bin histogram.
+__device__ int kth_from_hist(const uint32_t* h, int64_t k) {
+  int64_t c = 0;
+  for (int v = 0; v < 256; ++v) {
+    c += h[v];
+    if (c > k) return v;
+  }
+  return 255;
+}
+
+// np.percentile(float32 image, 95) with method 'linear' (numpy 2.x _quantile/_lerp, float32).
+__device__ float percentile95_from_hist(const uint32_t* h, int64_t n) {
+  const float q = 95.0f / 100.0f;                       // np.true_divide(95, float32(100))
+  const float vi = float(n - 1) * q;                    // (n-1) * quantiles, float32
+  float prev = floorf(vi);
+  float next = prev + 1.0f;
+  const float gamma = vi - prev;
+  int64_t pi = int64_t(prev), ni = int64_t(next);
+  if (vi >= float(n - 1)) { pi = n - 1; ni = n - 1; }   // index -1 -> last element
+  const float a = float(kth_from_hist(h, pi));
+  const float b = float(kth_from_hist(h, ni));
+  const float diff = b - a;
+  float r = a + diff * gamma;
+  if (gamma >= 0.5f) r = b - diff * (1.0f - gamma);
+  return r;
+}
+
+__global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
+  __shared__ uint32_t sh[3][256];
+  __shared__ uint32_t s_maxd;
+  __shared__ uint32_t s_last;
+  const int tid = threadIdx.x;
+  WsHeader* ws = p.ws;
+
+  // Arm the compaction state of the following main launch (ordered by the kernel boundary).
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + tid; i < p.n_state_words; i += int64_t(gridDim.x) * kBlock)
+    p.states[i] = 0;
+  if (blockIdx.x == 0 && tid == 0) ws->tile_counter = 0;
+
+  if (p.thresh_mode == SLG_THRESH_MANUAL) {
+    if (blockIdx.x == 0 && tid < 2) {
+      // smallest integer x with double(x) > thr, over the reachable range
+      const double thr = tid == 0 ? p.shadow_val : p.contrast_val;
+      const int lo = tid == 0 ? 0 : -255;
+      int m = 256;
+      for (int x = lo; x <= 256; ++x)
+        if (double(x) > thr) { m = x; break; }
+      if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
+    }
+    return;
+  }
+
+  for (int i = tid; i < 3 * 256; i += kBlock) (&sh[0][0])[i] = 0;
+  if (tid == 0) s_maxd = 0;
+  __syncthreads();
+
+  const bool otsu = p.thresh_mode == SLG_THRESH_OTSU;
+  uint32_t local_max = 0;
+  const int64_t n_chunks = (p.n_px + kPx - 1) / kPx;
+  for (int64_t c = int64_t(blockIdx.x) * kBlock + tid; c < n_chunks; c += int64_t(gridDim.x) * kBlock) {
+    const int64_t px0 = c * kPx;
+    const uint2 w = load8(p.white, px0, p.n_px);
+    const uint2 b = load8(p.black, px0, p.n_px);
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      if (px0 + k >= p.n_px) break;
+      const int wv = ((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 0xff;
+      const int bv = ((k < 4 ? b.x : b.y) >> (8 * (k & 3))) & 0xff;
+      const int d = wv - bv;
+      if (otsu) {
+        atomicAdd(&sh[0][wv], 1u);
+        atomicAdd(&sh[1][d < 0 ? 0 : d], 1u);
+      } else {
+        atomicAdd(&sh[2][bv], 1u);
+        local_max = max(local_max, uint32_t(d + 256));
+      }
+    }
+  }
+  if (!otsu) atomicMax(&s_maxd, local_max);
+  __syncthreads();
+  for (int i = tid; i < 3 * 256; i += kBlock) {
+    const uint32_t v = (&sh[0][0])[i];
+    if (v) atomicAdd(&(&ws->hist[0][0])[i], v);
+  }
+  if (!otsu && tid == 0 && s_maxd) atomicMax(&ws->max_diff_enc, s_maxd);
+
+  // Publish (every wave drains its atomics, barrier, one release) then take a ticket.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(&ws->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == gridDim.x - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+
+  // Last arriver: acquire, read the global histograms, compute thresholds, reset for reuse.
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int i = tid; i < 3 * 256; i += kBlock)
+    (&sh[0][0])[i] = __hip_atomic_load(&(&ws->hist[0][0])[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) s_maxd = __hip_atomic_load(&ws->max_diff_enc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (tid < 2) {
+    double thr;
+    int lo;
+    if (otsu) {
+      thr = otsu_from_hist(sh[tid], p.n_px);               // tid 0: white, 1: clip(w-b)
+      lo = tid == 0 ? 0 : -255;
+    } else {
+      if (tid == 0) {
+        const float nf = percentile95_from_hist(sh[2], p.n_px);
+        thr = double(nf * 1.5f);                           // noise_floor * 1.5 (float32)
+        lo = 0;
+      } else {
+        const float dr = float(int(s_maxd) - 256);         // np.max(contrast)
+        thr = double(dr * 0.05f);                          // dynamic_range * 0.05 (float32)
+        lo = -255;
+      }
+    }
+    int m = 256;
+    for (int x = lo; x <= 256; ++x)
+      if (double(x) > thr) { m = x; break; }
+    if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
+  }
+  for (int i = tid; i < 3 * 256; i += kBlock) (&ws->hist[0][0])[i] = 0;
+  if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
+}
+
+// ------------------------------------------------------------------ main kernel
+struct MainParams {
+  // frames source
+  const uint8_t* frames;
+  int64_t stride;
+  // maps source
+  const int32_t* in_col;
+  const int32_t* in_row;
+  const uint8_t* in_mask;
+  // common
+  const uint8_t* texture;
+  int64_t n_px;
+  int32_t width;
+  // decode plan (frame index of first pattern, pairs to read, pre-shift, post-shift)
+  int32_t col_first, col_pairs, col_pre, col_post;
+  int32_t row_first, row_pairs, row_pre, row_post;
+  // maps output
+  int32_t* out_col;
+  int32_t* out_row;
+  uint8_t* out_mask;
+  // calibration
+  const double* rays;
+  double fx, fy, cx, cy;
+  double o0, o1, o2;
+  const double* pcol;
+  int32_t n_pcol;
+  const double* prow;
+  int32_t n_prow;
+  double tol;
+  // outputs
+  void* xyz;
+  uint8_t* bgr;
+  int64_t* count;
+  WsHeader* ws;
+  uint64_t* states;        // [2][n_tiles]
+  int64_t n_tiles;
+  void* scratch_xyz;       // row_mode 2 row cloud
+  uint8_t* scratch_bgr;
+};
+
+template <int SRC_FRAMES>
+__device__ inline void decode_axis(const MainParams& p, int first, int pairs, int pre, int post,
+                                   int64_t px0, uint32_t (&acc)[4]) {
+  acc[0] = acc[1] = acc[2] = acc[3] = 0u;
+  for (int b = 0; b < pairs; ++b) {
+    const uint8_t* fp = p.frames + int64_t(first + 2 * b) * p.stride;
+    const uint2 pv = load8(fp, px0, p.n_px);
+    const uint2 iv = load8(fp + p.stride, px0, p.n_px);
+    const uint32_t m0 = gt_u8x4(pv.x, iv.x);
+    const uint32_t m1 = gt_u8x4(pv.y, iv.y);
+    acc[0] = (acc[0] << 1) | ((m0 >> 7) & 0x00010001u);
+    acc[1] = (acc[1] << 1) | ((m0 >> 15) & 0x00010001u);
+    acc[2] = (acc[2] << 1) | ((m1 >> 7) & 0x00010001u);
+    acc[3] = (acc[3] << 1) | ((m1 >> 15) & 0x00010001u);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = gray2bin_x2(acc[j] << pre) << post;
+}
+
+// code of pixel k (0..7) from the packed accumulators
+__device__ inline int unpack_code(const uint32_t (&acc)[4], int k) {
+  const uint32_t a = acc[((k >> 2) << 1) | (k & 1)];
+  return int((a >> (16 * ((k >> 1) & 1))) & 0xffffu);
+}
+
+struct Pt {
+  double x, y, z;
+};
+
+__device__ inline double ray_plane_denom(const double4& pl, double r0, double r1, double r2) {
+  return (pl.x * r0 + pl.y * r1) + pl.z * r2;                 // np.sum(N * rays, axis=0)
+}
+
+__device__ inline double4 load_plane(const double* tab, int n, int idx) {
+  idx = idx < 0 ? 0 : (idx > n - 1 ? n - 1 : idx);            // np.clip(idx, 0, n-1)
+  const double2* q = reinterpret_cast<const double2*>(tab + 4 * int64_t(idx));
+  const double2 a = q[0], b = q[1];
+  return make_double4(a.x, a.y, b.x, b.y);
+}
+
+template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int WRITE_MAPS, int TRI, int RAYS>
+__global__ __launch_bounds__(kBlock) void main_kernel(MainParams p) {
+  using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
+  constexpr int kStageXyz = TRI ? kTilePx * 3 : 1;
+  __shared__ XT s_xyz[kStageXyz];
+  __shared__ uint8_t s_bgr[TRI ? kTilePx * 3 : 4];
+  __shared__ int s_wave_tot[4];
+  __shared__ int s_tile;
+  __shared__ uint64_t s_excl;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+
+  int tile;
+  if (TRI) {
+    if (tid == 0) s_tile = int(atomicAdd(&p.ws->tile_counter, 1u));
+    __syncthreads();
+    tile = s_tile;
+  } else {
+    tile = blockIdx.x;
+  }
+  const int64_t px0 = int64_t(tile) * kTilePx + int64_t(tid) * kPx;
+
+  // -------------------------------------------------------------- decode 8 pixels
+  uint32_t valid = 0;   // bit k: mask of pixel k
+  int col[kPx], row[kPx];
+  if (SRC_FRAMES) {
+    const int smin = p.ws->smin, cmin = p.ws->cmin;
+    const uint2 w = load8(p.frames, px0, p.n_px);
+    const uint2 bl = load8(p.frames + p.stride, px0, p.n_px);
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      const int wv = ((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 0xff;
+      const int bv = ((k < 4 ? bl.x : bl.y) >> (8 * (k & 3))) & 0xff;
+      const bool ok = (wv >= smin) & ((wv - bv) >= cmin) & (px0 + k < p.n_px);
+      valid |= uint32_t(ok) << k;
+    }
+    uint32_t acc[4];
+    decode_axis<1>(p, p.col_first, p.col_pairs, p.col_pre, p.col_post, px0, acc);
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) col[k] = unpack_code(acc, k);
+    if (ROW_MODE != 0 || WRITE_MAPS) {
+      decode_axis<1>(p, p.row_first, p.row_pairs, p.row_pre, p.row_post, px0, acc);
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) row[k] = unpack_code(acc, k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) row[k] = 0;
+    }
+    if (WRITE_MAPS) {
+      if (px0 + kPx <= p.n_px) {
+        int4* oc = reinterpret_cast<int4*>(p.out_col + px0);
+        int4* orr = reinterpret_cast<int4*>(p.out_row + px0);
+        oc[0] = make_int4(col[0], col[1], col[2], col[3]);
+        oc[1] = make_int4(col[4], col[5], col[6], col[7]);
+        orr[0] = make_int4(row[0], row[1], row[2], row[3]);
+        orr[1] = make_int4(row[4], row[5], row[6], row[7]);
+        uint32_t m0 = 0, m1 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          m0 |= ((valid >> k) & 1u) << (8 * k);
+          m1 |= ((valid >> (k + 4)) & 1u) << (8 * k);
+        }
+        *reinterpret_cast<uint2*>(p.out_mask + px0) = make_uint2(m0, m1);
+      } else {
+        for (int k = 0; k < kPx; ++k)
+          if (px0 + k < p.n_px) {
+            p.out_col[px0 + k] = col[k];
+            p.out_row[px0 + k] = row[k];
+            p.out_mask[px0 + k] = uint8_t((valid >> k) & 1u);
+          }
+      }
+    }
+  } else {
+    if (px0 + kPx <= p.n_px) {
+      const int4* ic = reinterpret_cast<const int4*>(p.in_col + px0);
+      const int4 c0 = ic[0], c1 = ic[1];
+      col[0] = c0.x; col[1] = c0.y; col[2] = c0.z; col[3] = c0.w;
+      col[4] = c1.x; col[5] = c1.y; col[6] = c1.z; col[7] = c1.w;
+      if (ROW_MODE != 0) {
+        const int4* ir = reinterpret_cast<const int4*>(p.in_row + px0);
+        const int4 r0 = ir[0], r1 = ir[1];
+        row[0] = r0.x; row[1] = r0.y; row[2] = r0.z; row[3] = r0.w;
+        row[4] = r1.x; row[5] = r1.y; row[6] = r1.z; row[7] = r1.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) row[k] = 0;
+      }
+      const uint2 mv = *reinterpret_cast<const uint2*>(p.in_mask + px0);
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) valid |= uint32_t((((k < 4 ? mv.x : mv.y) >> (8 * (k & 3))) & 0xff) != 0) << k;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {
+        const bool in = px0 + k < p.n_px;
+        col[k] = in ? p.in_col[px0 + k] : 0;
+        row[k] = (in && ROW_MODE != 0) ? p.in_row[px0 + k] : 0;
+        valid |= uint32_t(in && p.in_mask[px0 + k] != 0) << k;
+      }
+    }
+  }
+  if (!TRI) return;
+
+  // -------------------------------------------------------------- triangulate
+  uint32_t keep_c = 0, keep_r = 0;
+  XT xc[kPx][3], xr[ROW_MODE == 2 ? kPx : 1][3];
+  uint32_t tex[6] = {0, 0, 0, 0, 0, 0};   // 24 bytes BGR of the 8 pixels
+  if (valid) {
+    const int64_t tb = px0 * 3;
+    if (px0 + kPx <= p.n_px) {
+      const uint2* tq = reinterpret_cast<const uint2*>(p.texture + tb);
+      const uint2 t0 = tq[0], t1 = tq[1], t2 = tq[2];
+      tex[0] = t0.x; tex[1] = t0.y; tex[2] = t1.x; tex[3] = t1.y; tex[4] = t2.x; tex[5] = t2.y;
+    } else {
+      for (int k = 0; k < 3 * kPx; ++k)
+        if (px0 * 3 + k < p.n_px * 3) tex[k >> 2] |= uint32_t(p.texture[tb + k]) << (8 * (k & 3));
+    }
+    int v = int(px0 / p.width);
+    int u = int(px0 - int64_t(v) * p.width);
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      if (valid & (1u << k)) {
+        double r0, r1, r2;
+        if (RAYS == SLG_RAYS_PINHOLE) {
+          const double x = (double(u) - p.cx) / p.fx;           // processing.py:150
+          const double y = (double(v) - p.cy) / p.fy;           // processing.py:151
+          const double n = sqrt((x * x + y * y) + 1.0);         // np.linalg.norm(axis=0)
+          r0 = x / n; r1 = y / n; r2 = 1.0 / n;                 // rays /= norms
+        } else {
+          const int64_t px = px0 + k;
+          r0 = p.rays[px];
+          r1 = p.rays[p.n_px + px];
+          r2 = p.rays[2 * p.n_px + px];
+        }
+        const double4 pc = load_plane(p.pcol, p.n_pcol, col[k]);
+        const double den = ray_plane_denom(pc, r0, r1, r2);
+        const double num = ((pc.x * p.o0 + pc.y * p.o1) + pc.z * p.o2) + pc.w;
+        const bool okc = fabs(den) > 1e-6;
+        const double t = okc ? (-num) / den : 0.0;
+        const double X = p.o0 + r0 * t, Y = p.o1 + r1 * t, Z = p.o2 + r2 * t;
+        bool kc = okc;
+        if constexpr (ROW_MODE == 1) {
+          const double4 pr = load_plane(p.prow, p.n_prow, row[k]);
+          const double dist = fabs(((pr.x * X + pr.y * Y) + pr.z * Z) + pr.w);
+          kc = okc && (dist < p.tol);
+        }
+        if (kc) {
+          keep_c |= 1u << k;
+          xc[k][0] = XT(X); xc[k][1] = XT(Y); xc[k][2] = XT(Z);
+        }
+        if constexpr (ROW_MODE == 2) {
+          const double4 pr = load_plane(p.prow, p.n_prow, row[k]);
+          const double dr = ray_plane_denom(pr, r0, r1, r2);
+          const double nr = ((pr.x * p.o0 + pr.y * p.o1) + pr.z * p.o2) + pr.w;
+          if (fabs(dr) > 1e-6) {
+            const double tr = (-nr) / dr;
+            keep_r |= 1u << k;
+            xr[k][0] = XT(p.o0 + r0 * tr); xr[k][1] = XT(p.o1 + r1 * tr); xr[k][2] = XT(p.o2 + r2 * tr);
+          }
+        }
+      }
+      if (++u == p.width) { u = 0; ++v; }
+    }
+  }
+
+  // -------------------------------------------------------------- ordered compaction
+#pragma unroll 1
+  for (int stream = 0; stream < (ROW_MODE == 2 ? 2 : 1); ++stream) {
+    const uint32_t keep = stream == 0 ? keep_c : keep_r;
+    const int cnt = __popc(keep);
+    // inclusive wave scan
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_wave_tot[wave] = incl;
+    __syncthreads();
+    int wave_off = 0, agg = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      wave_off += (w < wave) ? s_wave_tot[w] : 0;
+      agg += s_wave_tot[w];
+    }
+    const int local = wave_off + incl - cnt;
+
+    // stage the lane's points into LDS at their compacted slot
+    {
+      int j = local;
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {
+        if (keep & (1u << k)) {
+          if constexpr (ROW_MODE == 2) {
+            const XT* src = stream == 0 ? xc[k] : xr[k];
+            s_xyz[3 * j + 0] = src[0]; s_xyz[3 * j + 1] = src[1]; s_xyz[3 * j + 2] = src[2];
+          } else {
+            s_xyz[3 * j + 0] = xc[k][0]; s_xyz[3 * j + 1] = xc[k][1]; s_xyz[3 * j + 2] = xc[k][2];
+          }
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int bi = 3 * k + c;
+            s_bgr[3 * j + c] = uint8_t((tex[bi >> 2] >> (8 * (bi & 3))) & 0xff);
+          }
+          ++j;
+        }
+      }
+    }
+
+    // tile prefix: decoupled look-back by wave 0
+    uint64_t* st = p.states + int64_t(stream) * p.n_tiles;
+    if (wave == 0) {
+      uint64_t excl = 0;
+      if (tile == 0) {
+        if (lane == 0) st_state(&st[0], kFlagInc | uint64_t(agg));
+      } else {
+        if (lane == 0) st_state(&st[tile], kFlagAgg | uint64_t(agg));
+        int64_t j = tile - 1;
+        for (;;) {
+          uint64_t vv[kLookK];
+#pragma unroll
+          for (int k = 0; k < kLookK; ++k) {
+            const int64_t s = j - (k * 64 + lane);
+            vv[k] = s >= 0 ? ld_state(&st[s]) : kFlagInc;
+          }
+          unsigned spins = 0;
+          for (;;) {
+            bool ready = true;
+#pragma unroll
+            for (int k = 0; k < kLookK; ++k) ready &= (vv[k] >> 62) != 0;
+            if (__all(ready)) break;
+            if (++spins > kMaxSpin) {
+              if (lane == 0) atomicOr(&p.ws->error, 1u);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int k = 0; k < kLookK; ++k) {
+              const int64_t s = j - (k * 64 + lane);
+              if ((vv[k] >> 62) == 0 && s >= 0) vv[k] = ld_state(&st[s]);
+            }
+          }
+          int my_pos = INT_MAX;
+#pragma unroll
+          for (int k = kLookK - 1; k >= 0; --k)
+            if ((vv[k] >> 62) == 2) my_pos = k * 64 + lane;
+          const int pos = wave_min_i(my_pos);
+          uint64_t sum = 0;
+#pragma unroll
+          for (int k = 0; k < kLookK; ++k)
+            if (k * 64 + lane <= pos) sum += vv[k] & kValMask;
+          excl += wave_sum(sum);
+          if (pos != INT_MAX) break;
+          j -= kLookK * 64;
+        }
+        if (lane == 0) st_state(&st[tile], kFlagInc | (excl + uint64_t(agg)));
+      }
+      if (lane == 0) {
+        s_excl = excl;
+        if (tile == p.n_tiles - 1) {
+          p.ws->totals[stream] = int64_t(excl) + agg;
+          if (ROW_MODE != 2) *p.count = int64_t(excl) + agg;
+        }
+      }
+    }
+    __syncthreads();
+    const int64_t base = int64_t(s_excl);
+
+    // coalesced copy-out of the tile's compacted points
+    XT* gx = reinterpret_cast<XT*>(stream == 0 ? p.xyz : p.scratch_xyz) + base * 3;
+    for (int i = tid; i < agg * 3; i += kBlock) gx[i] = s_xyz[i];
+    uint8_t* gb = (stream == 0 ? p.bgr : p.scratch_bgr);
+    const int64_t lo = base * 3, hi = (base + agg) * 3;
+    const int64_t lo4 = (lo + 3) & ~int64_t(3), hi4 = hi & ~int64_t(3);
+    if (lo4 < hi4) {
+      for (int64_t i = lo4 + 4 * int64_t(tid); i < hi4; i += 4 * kBlock) {
+        const int64_t s = i - lo;
+        const uint32_t v = uint32_t(s_bgr[s]) | (uint32_t(s_bgr[s + 1]) << 8) |
+                           (uint32_t(s_bgr[s + 2]) << 16) | (uint32_t(s_bgr[s + 3]) << 24);
+        *reinterpret_cast<uint32_t*>(gb + i) = v;
+      }
+      if (tid < lo4 - lo) gb[lo + tid] = s_bgr[tid];
+      if (tid < hi - hi4) gb[hi4 + tid] = s_bgr[hi4 - lo + tid];
+    } else {
+      for (int64_t i = lo + tid; i < hi; i += kBlock) gb[i] = s_bgr[i - lo];
+    }
+    __syncthreads();   // LDS reuse by the next stream
+  }
+}
+
+// row_mode 2: append the row cloud (workspace scratch) behind the column cloud.
+template <int XYZ64>
+__global__ __launch_bounds__(kBlock) void row_tail_kernel(WsHeader* ws, const void* sx, const uint8_t* sb,
+                                                          void* xyz, uint8_t* bgr, int64_t* count) {
+  using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
+  const int64_t nc = ws->totals[0], nr = ws->totals[1];
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i == 0) *count = nc + nr;
+  if (i >= nr) return;
+  const XT* s = reinterpret_cast<const XT*>(sx);
+  XT* d = reinterpret_cast<XT*>(xyz);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    d[(nc + i) * 3 + c] = s[i * 3 + c];
+    bgr[(nc + i) * 3 + c] = sb[i * 3 + c];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void pinhole_kernel(const double* rays, int64_t n_px, int width, double fx,
+                                                         double fy, double cx, double cy,
+                                                         unsigned long long* mismatches) {
+  const int64_t px = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  unsigned bad = 0;
+  if (px < n_px) {
+    const int v = int(px / width), u = int(px - int64_t(v) * width);
+    const double x = (double(u) - cx) / fx;
+    const double y = (double(v) - cy) / fy;
+    const double n = sqrt((x * x + y * y) + 1.0);
+    const double r[3] = {x / n, y / n, 1.0 / n};
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      bad += __double_as_longlong(r[c]) != __double_as_longlong(rays[c * n_px + px]);
+  }
+  bad = wave_sum(bad);
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(mismatches, (unsigned long long)bad);
+}
+
+// ------------------------------------------------------------------ host side
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(SLG_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+  return SLG_OK;
+}
+
+int ceil_log2(int n) {
+  int b = 0;
+  while ((1ll << b) < (long long)n) ++b;
+  return b;
+}
+
+struct Plan {
+  int col_first, col_pairs, col_pre, col_post;
+  int row_first, row_pairs, row_pre, row_post;
+};
+
+// Which frames each axis reads and how the code is shifted (processing.py:80-122,
+// sl_system.py:546-585).
+int make_plan(const slg_capture* cap, const slg_decode_params* dp, Plan* pl) {
+  if (cap->n_frames < 4)
+    return fail(SLG_ERR_NOT_ENOUGH, "Not enough images (got %d, need at least 4).", cap->n_frames);
+  if (dp->proj_cols < 1 || dp->proj_rows < 1) return fail(SLG_ERR_INVALID, "projector size must be positive");
+  const int Bc = ceil_log2(dp->proj_cols), Br = ceil_log2(dp->proj_rows);
+  if (Bc > kMaxBits || Br > kMaxBits)
+    return fail(SLG_ERR_UNSUPPORTED, "at most %d code bits per axis (got %d, %d)", kMaxBits, Bc, Br);
+  const int n = cap->n_frames;
+  if (dp->variant == SLG_VARIANT_PROCESSING) {
+    const int nc = dp->n_sets_col < 1 ? 1 : (dp->n_sets_col > Bc ? Bc : dp->n_sets_col);
+    const int nr = dp->n_sets_row < 1 ? 1 : (dp->n_sets_row > Br ? Br : dp->n_sets_row);
+    int kc = 0, kr = 0;
+    for (int b = 0; b < nc; ++b) kc += (2 + 2 * b + 1 < n);          // processing.py:94
+    for (int b = 0; b < nr; ++b) kr += (2 + 2 * Bc + 2 * b + 1 < n);
+    *pl = {2, kc, nc - kc, Bc - nc, 2 + 2 * Bc, kr, nr - kr, Br - nr};
+  } else if (dp->variant == SLG_VARIANT_SLSYSTEM) {
+    int idx = 2, kc = 0, kr = 0;
+    for (int b = 0; b < Bc; ++b) {                                  // sl_system.py:557-562
+      if (idx >= n) break;
+      if (idx + 1 >= n) return fail(SLG_ERR_INDEX, "list index out of range");
+      idx += 2; ++kc;
+    }
+    const int row_first = idx;
+    for (int b = 0; b < Br; ++b) {
+      if (idx >= n) break;
+      if (idx + 1 >= n) return fail(SLG_ERR_INDEX, "list index out of range");
+      idx += 2; ++kr;
+    }
+    *pl = {2, kc, Bc - kc, 0, row_first, kr, Br - kr, 0};
+  } else {
+    return fail(SLG_ERR_INVALID, "unknown variant %d", dp->variant);
+  }
+  return SLG_OK;
+}
+
+int check_capture(const slg_capture* cap) {
+  if (!cap || !cap->frames) return fail(SLG_ERR_INVALID, "capture frames is NULL");
+  if (cap->height < 1 || cap->width < 1) return fail(SLG_ERR_INVALID, "bad image size %dx%d", cap->width, cap->height);
+  const int64_t n_px = int64_t(cap->height) * cap->width;
+  if (n_px >= (int64_t(1) << 31)) return fail(SLG_ERR_UNSUPPORTED, "image larger than 2^31 pixels");
+  if (cap->frame_stride < n_px || (cap->frame_stride & 7)) return fail(SLG_ERR_INVALID, "frame_stride must be >= H*W and a multiple of 8");
+  if (reinterpret_cast<uintptr_t>(cap->frames) & 7) return fail(SLG_ERR_INVALID, "frames must be 8-byte aligned");
+  return SLG_OK;
+}
+
+int stats_launch(const uint8_t* white, const uint8_t* black, int64_t n_px, const slg_decode_params* dp,
+                 void* workspace, hipStream_t s) {
+  StatsParams sp{};
+  sp.white = white;
+  sp.black = black;
+  sp.n_px = n_px;
+  sp.ws = reinterpret_cast<WsHeader*>(workspace);
+  sp.states = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + states_off(n_px));
+  sp.n_state_words = 2 * n_tiles_of(n_px);
+  sp.thresh_mode = dp ? dp->thresh_mode : SLG_THRESH_MANUAL;
+  sp.shadow_val = dp ? dp->shadow_val : 0.0;
+  sp.contrast_val = dp ? dp->contrast_val : 0.0;
+  const int64_t chunks = (n_px + kPx - 1) / kPx;
+  int64_t grid = (chunks + kBlock - 1) / kBlock;
+  if (grid > 1024) grid = 1024;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(stats_kernel, dim3(unsigned(grid)), dim3(kBlock), 0, s, sp);
+  return check_launch("stats_kernel");
+}
+
+using MainFn = void (*)(MainParams);
+
+template <int RM, int X64, int SRC, int WM, int RAYS>
+MainFn pick5() { return main_kernel<RM, X64, SRC, WM, 1, RAYS>; }
+
+template <int SRC, int WM>
+MainFn pick_tri(int row_mode, int x64, int rays) {
+#define SLG_CASE(RM, X, R) if (row_mode == RM && x64 == X && rays == R) return pick5<RM, X, SRC, WM, R>();
+  SLG_CASE(0, 0, 0) SLG_CASE(0, 0, 1) SLG_CASE(0, 1, 0) SLG_CASE(0, 1, 1)
+  SLG_CASE(1, 0, 0) SLG_CASE(1, 0, 1) SLG_CASE(1, 1, 0) SLG_CASE(1, 1, 1)
+  SLG_CASE(2, 0, 0) SLG_CASE(2, 0, 1) SLG_CASE(2, 1, 0) SLG_CASE(2, 1, 1)
+#undef SLG_CASE
+  return nullptr;
+}
+
+int fill_calib(MainParams& mp, const slg_calib* c, const slg_tri_params* tp, int64_t n_px, int width) {
+  if (!c || !tp) return fail(SLG_ERR_INVALID, "calib/tri params NULL");
+  if (tp->row_mode < 0 || tp->row_mode > 2) return fail(SLG_ERR_INVALID, "row_mode must be 0, 1 or 2");
+  if (c->ray_mode == SLG_RAYS_TABLE && !c->rays) return fail(SLG_ERR_INVALID, "ray table is NULL");
+  if (c->ray_mode != SLG_RAYS_TABLE && c->ray_mode != SLG_RAYS_PINHOLE) return fail(SLG_ERR_INVALID, "bad ray_mode");
+  if (!c->col_planes || c->n_col_planes < 1) return fail(SLG_ERR_INVALID, "column planes missing");
+  if (tp->row_mode != 0 && (!c->row_planes || c->n_row_planes < 1)) return fail(SLG_ERR_INVALID, "row planes missing");
+  if ((reinterpret_cast<uintptr_t>(c->col_planes) | reinterpret_cast<uintptr_t>(c->row_planes)) & 15)
+    return fail(SLG_ERR_INVALID, "plane tables must be 16-byte aligned");
+  mp.rays = c->rays;
+  mp.fx = c->fx; mp.fy = c->fy; mp.cx = c->cx; mp.cy = c->cy;
+  mp.o0 = c->oc[0]; mp.o1 = c->oc[1]; mp.o2 = c->oc[2];
+  mp.pcol = c->col_planes; mp.n_pcol = c->n_col_planes;
+  mp.prow = c->row_planes; mp.n_prow = c->n_row_planes;
+  mp.tol = tp->epipolar_tol;
+  mp.n_px = n_px;
+  mp.width = width;
+  return SLG_OK;
+}
+
+int fill_out(MainParams& mp, const slg_cloud* out, const slg_tri_params* tp, int64_t n_px, void* ws) {
+  if (!out || !out->xyz || !out->bgr || !out->count) return fail(SLG_ERR_INVALID, "output cloud buffers NULL");
+  const int64_t need = tp->row_mode == 2 ? 2 * n_px : n_px;
+  if (out->capacity < need) return fail(SLG_ERR_INVALID, "cloud capacity %lld < %lld", (long long)out->capacity, (long long)need);
+  mp.xyz = out->xyz;
+  mp.bgr = out->bgr;
+  mp.count = out->count;
+  mp.ws = reinterpret_cast<WsHeader*>(ws);
+  mp.states = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + states_off(n_px));
+  mp.n_tiles = n_tiles_of(n_px);
+  mp.scratch_xyz = static_cast<char*>(ws) + scratch_xyz_off(n_px);
+  mp.scratch_bgr = reinterpret_cast<uint8_t*>(static_cast<char*>(ws) + scratch_bgr_off(n_px));
+  return SLG_OK;
+}
+
+int launch_main(MainFn fn, const MainParams& mp, const slg_tri_params* tp, const slg_cloud* out, hipStream_t s) {
+  if (!fn) return fail(SLG_ERR_INVALID, "no kernel for this configuration");
+  hipLaunchKernelGGL(fn, dim3(unsigned(mp.n_tiles)), dim3(kBlock), 0, s, mp);
+  int rc = check_launch("main_kernel");
+  if (rc) return rc;
+  if (tp && tp->row_mode == 2) {
+    const unsigned grid = unsigned((mp.n_px + kBlock - 1) / kBlock);
+    if (tp->xyz_f64)
+      hipLaunchKernelGGL(row_tail_kernel<1>, dim3(grid), dim3(kBlock), 0, s, mp.ws, mp.scratch_xyz, mp.scratch_bgr, out->xyz, out->bgr, out->count);
+    else
+      hipLaunchKernelGGL(row_tail_kernel<0>, dim3(grid), dim3(kBlock), 0, s, mp.ws, mp.scratch_xyz, mp.scratch_bgr, out->xyz, out->bgr, out->count);
+    rc = check_launch("row_tail_kernel");
+  }
+  return rc;
+}
+
+}  // namespace
+
+// ==================================================================== C ABI
+extern "C" {
+
+int32_t slg_version(void) { return SLG_ABI_VERSION; }
+
+const char* slg_last_error(void) { return g_err; }
+
+int64_t slg_workspace_bytes(int64_t n_pixels) { return n_pixels > 0 ? ws_total(n_pixels) : kHeaderBytes; }
+
+int32_t slg_workspace_init(void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!workspace) return fail(SLG_ERR_INVALID, "workspace NULL");
+  const int64_t n = workspace_bytes < kHeaderBytes ? workspace_bytes : kHeaderBytes;
+  if (hipMemsetAsync(workspace, 0, size_t(n), static_cast<hipStream_t>(stream)) != hipSuccess)
+    return fail(SLG_ERR_HIP, "hipMemsetAsync failed");
+  return SLG_OK;
+}
+
+int32_t slg_decode_stats(const slg_capture* cap, const slg_decode_params* dp, void* workspace, void* stream) {
+  int rc = check_capture(cap);
+  if (rc) return rc;
+  if (!dp || !workspace) return fail(SLG_ERR_INVALID, "NULL argument");
+  if (cap->n_frames < 4)
+    return fail(SLG_ERR_NOT_ENOUGH, "Not enough images (got %d, need at least 4).", cap->n_frames);
+  if (dp->thresh_mode < 0 || dp->thresh_mode > 2) return fail(SLG_ERR_INVALID, "bad thresh_mode");
+  const int64_t n_px = int64_t(cap->height) * cap->width;
+  return stats_launch(cap->frames, cap->frames + cap->frame_stride, n_px, dp, workspace,
+                      static_cast<hipStream_t>(stream));
+}
+
+int32_t slg_decode(const slg_capture* cap, const slg_decode_params* dp, void* workspace, int32_t* col_out,
+                   int32_t* row_out, uint8_t* mask_out, void* stream) {
+  int rc = check_capture(cap);
+  if (rc) return rc;
+  if (!dp || !workspace || !col_out || !row_out || !mask_out) return fail(SLG_ERR_INVALID, "NULL argument");
+  if ((reinterpret_cast<uintptr_t>(col_out) | reinterpret_cast<uintptr_t>(row_out)) & 15 ||
+      reinterpret_cast<uintptr_t>(mask_out) & 7)
+    return fail(SLG_ERR_INVALID, "map outputs must be 16-byte (col,row) / 8-byte (mask) aligned");
+  Plan pl;
+  rc = make_plan(cap, dp, &pl);
+  if (rc) return rc;
+  const int64_t n_px = int64_t(cap->height) * cap->width;
+  MainParams mp{};
+  mp.frames = cap->frames;
+  mp.stride = cap->frame_stride;
+  mp.n_px = n_px;
+  mp.width = cap->width;
+  mp.col_first = pl.col_first; mp.col_pairs = pl.col_pairs; mp.col_pre = pl.col_pre; mp.col_post = pl.col_post;
+  mp.row_first = pl.row_first; mp.row_pairs = pl.row_pairs; mp.row_pre = pl.row_pre; mp.row_post = pl.row_post;
+  mp.out_col = col_out; mp.out_row = row_out; mp.out_mask = mask_out;
+  mp.ws = reinterpret_cast<WsHeader*>(workspace);
+  mp.n_tiles = n_tiles_of(n_px);
+  hipLaunchKernelGGL((main_kernel<0, 0, 1, 1, 0, 0>), dim3(unsigned(mp.n_tiles)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), mp);
+  return check_launch("decode main_kernel");
+}
+
+int32_t slg_triangulate(const slg_maps* maps, const slg_calib* calib, const slg_tri_params* tp, void* workspace,
+                        const slg_cloud* out, void* stream) {
+  if (!maps || !maps->col || !maps->mask || !maps->texture || !workspace) return fail(SLG_ERR_INVALID, "NULL argument");
+  if (maps->height < 1 || maps->width < 1) return fail(SLG_ERR_INVALID, "bad map size");
+  if (tp && tp->row_mode != 0 && !maps->row) return fail(SLG_ERR_INVALID, "row map required for row_mode 1/2");
+  if ((reinterpret_cast<uintptr_t>(maps->col) | reinterpret_cast<uintptr_t>(maps->row)) & 15 ||
+      (reinterpret_cast<uintptr_t>(maps->mask) | reinterpret_cast<uintptr_t>(maps->texture)) & 7)
+    return fail(SLG_ERR_INVALID, "maps must be 16-byte (col,row) / 8-byte (mask,texture) aligned");
+  const int64_t n_px = int64_t(maps->height) * maps->width;
+  MainParams mp{};
+  int rc = fill_calib(mp, calib, tp, n_px, maps->width);
+  if (rc) return rc;
+  rc = fill_out(mp, out, tp, n_px, workspace);
+  if (rc) return rc;
+  mp.in_col = maps->col; mp.in_row = maps->row; mp.in_mask = maps->mask; mp.texture = maps->texture;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  rc = stats_launch(nullptr, nullptr, n_px, nullptr, workspace, s);   // arms states only (manual mode)
+  if (rc) return rc;
+  return launch_main(pick_tri<0, 0>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode), mp, tp, out, s);
+}
+
+int32_t slg_reconstruct(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,
+                        const slg_tri_params* tp, void* workspace, const slg_cloud* out, void* stream) {
+  int rc = check_capture(cap);
+  if (rc) return rc;
+  if (!dp || !workspace || !cap->texture) return fail(SLG_ERR_INVALID, "NULL argument");
+  if (reinterpret_cast<uintptr_t>(cap->texture) & 7) return fail(SLG_ERR_INVALID, "texture must be 8-byte aligned");
+  Plan pl;
+  rc = make_plan(cap, dp, &pl);
+  if (rc) return rc;
+  const int64_t n_px = int64_t(cap->height) * cap->width;
+  MainParams mp{};
+  rc = fill_calib(mp, calib, tp, n_px, cap->width);
+  if (rc) return rc;
+  rc = fill_out(mp, out, tp, n_px, workspace);
+  if (rc) return rc;
+  mp.frames = cap->frames;
+  mp.stride = cap->frame_stride;
+  mp.texture = cap->texture;
+  mp.col_first = pl.col_first; mp.col_pairs = pl.col_pairs; mp.col_pre = pl.col_pre; mp.col_post = pl.col_post;
+  mp.row_first = pl.row_first; mp.row_pairs = pl.row_pairs; mp.row_pre = pl.row_pre; mp.row_post = pl.row_post;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  rc = stats_launch(cap->frames, cap->frames + cap->frame_stride, n_px, dp, workspace, s);
+  if (rc) return rc;
+  return launch_main(pick_tri<1, 0>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode), mp, tp, out, s);
+}
+
+int32_t slg_rays_match_pinhole(const double* rays, int32_t height, int32_t width, double fx, double fy, double cx,
+                               double cy, int64_t* mismatches, void* stream) {
+  if (!rays || !mismatches || height < 1 || width < 1) return fail(SLG_ERR_INVALID, "bad argument");
+  const int64_t n_px = int64_t(height) * width;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(mismatches, 0, sizeof(int64_t), s) != hipSuccess) return fail(SLG_ERR_HIP, "hipMemsetAsync failed");
+  hipLaunchKernelGGL(pinhole_kernel, dim3(unsigned((n_px + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rays, n_px,
+                     int(width), fx, fy, cx, cy, reinterpret_cast<unsigned long long*>(mismatches));
+  return check_launch("pinhole_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,264 @@
+"""Device-resident reconstruction engine: HBM frame stacks, calibration tables and the calls
+into ``libslgpu.so``.  PyTorch provides device memory and the current HIP stream only.
+
+Data layout in HBM:
+* frames  uint8 [F, stride], stride = round_up(H*W, 16): planar, one frame per row, in the
+          reference's capture order (``server/sl_system.py:444-459``);
+* texture uint8 [H*W, 3] BGR;
+* planes  float64 [P, 4] row-major (``wPlaneCol.T`` / ``wPlaneRow.T``);
+* rays    float64 [3, H*W] only when ``Nc`` is not the pinhole table (else recomputed);
+* cloud   float32|float64 [cap, 3] XYZ + uint8 [cap, 3] BGR + int64 count, ascending pixel order.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+
+def _vp(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def default_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("structured_light_for_3d_model_replication_amd needs a ROCm GPU "
+                           "(no CPU fallback in the product path)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def n_bits(n: int) -> int:
+    """``int(np.ceil(np.log2(n)))`` (server/processing.py:80-81)."""
+    return int(np.ceil(np.log2(n)))
+
+
+def weak_scalar(x) -> float:
+    """Value a NumPy-2 comparison ``float32_array > x`` uses (NEP 50): Python scalars are cast
+    to float32, NumPy scalars keep their own (wider) type."""
+    if isinstance(x, np.generic):
+        return float(x)
+    return float(np.float32(x))
+
+
+# ----------------------------------------------------------------------------- frames
+class DeviceFrames:
+    """A capture's frame stack in HBM (``uint8 [F, stride]``) plus its BGR texture."""
+
+    def __init__(self, frames, texture=None, device=None, n_frames=None):
+        """``frames``: uint8 tensor [F,H,W] (any device) or a sequence of HxW arrays in capture
+        order; ``None`` entries are frames the decode will not read (left unset in HBM)."""
+        device = device or default_device()
+        if isinstance(frames, torch.Tensor) and frames.dim() == 3:
+            F, H, W = frames.shape
+            frames_iter = None
+        else:
+            frames_iter = list(frames)
+            F = len(frames_iter)
+            first = next((f for f in frames_iter if f is not None), None)
+            if first is None:
+                raise ValueError(f"Not enough images (got {F}, need at least 4).")
+            H, W = np.asarray(first).shape[:2]
+        self.height, self.width, self.n_px = int(H), int(W), int(H) * int(W)
+        self.n_frames = int(F if n_frames is None else n_frames)
+        self.stride = (self.n_px + 15) // 16 * 16
+        self.data = torch.empty((max(F, 2), self.stride), dtype=torch.uint8, device=device)
+        if frames_iter is None:
+            self.data[:F, : self.n_px].copy_(frames.reshape(F, -1))
+        else:
+            for k, fr in enumerate(frames_iter):
+                if fr is None:
+                    continue
+                a = np.ascontiguousarray(fr, dtype=np.uint8).reshape(-1)
+                if a.size != self.n_px:
+                    raise ValueError("all frames must have the same size")
+                self.data[k, : self.n_px].copy_(torch.from_numpy(a))
+        if texture is None:
+            t0 = frames[0] if frames_iter is None else frames_iter[0]
+            t0 = t0.cpu().numpy() if isinstance(t0, torch.Tensor) else np.asarray(t0)
+            texture = np.repeat(t0[..., None], 3, axis=-1)
+        if isinstance(texture, torch.Tensor):
+            self.texture = texture.reshape(self.n_px, 3).to(device=device, dtype=torch.uint8).contiguous()
+        else:
+            tex = np.ascontiguousarray(texture, dtype=np.uint8).reshape(self.n_px, 3)
+            self.texture = torch.from_numpy(tex).to(device)
+
+    def capture(self) -> N.Capture:
+        return N.Capture(frames=self.data.data_ptr(), frame_stride=self.stride,
+                         n_frames=self.n_frames, height=self.height, width=self.width,
+                         reserved=0, texture=self.texture.data_ptr())
+
+
+# ----------------------------------------------------------------------------- calibration
+def _plane_table(tab) -> np.ndarray:
+    tab = np.asarray(tab, dtype=np.float64)
+    if tab.shape[0] == 4:                           # server/processing.py:134,186
+        tab = tab.T
+    return np.ascontiguousarray(tab[:, :4])
+
+
+class DeviceCalib:
+    """Calibration tables in HBM for one camera geometry.
+
+    Ray source follows ``server/processing.py:143-156``: ``Nc`` is used when it has one column
+    per pixel, else rays are recomputed from ``cam_K``.  A full-size ``Nc`` that is bitwise
+    equal to the ``cam_K`` pinhole rays (what ``calibrate_final`` writes) is not kept: the
+    kernels recompute the identical values, saving 24 B per pixel of HBM traffic.
+    """
+
+    def __init__(self, calib: dict, height: int, width: int, device=None, keep_table=False):
+        device = device or default_device()
+        self.height, self.width = int(height), int(width)
+        K = np.asarray(calib["cam_K"], dtype=np.float64)
+        self.fx, self.fy, self.cx, self.cy = float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2])
+        self.oc = np.asarray(calib["Oc"], dtype=np.float64).reshape(-1)[:3]
+        self.col_planes = torch.from_numpy(_plane_table(calib["wPlaneCol"])).to(device)
+        self.row_planes = (torch.from_numpy(_plane_table(calib["wPlaneRow"])).to(device)
+                           if "wPlaneRow" in calib and calib["wPlaneRow"] is not None else None)
+        Nc = np.asarray(calib["Nc"])
+        self.rays = None
+        self.ray_mode = N.RAYS_PINHOLE
+        self.table_is_pinhole = None
+        if Nc.ndim == 2 and Nc.shape[1] == self.height * self.width:
+            rays = torch.from_numpy(np.ascontiguousarray(Nc, dtype=np.float64)).to(device)
+            mism = torch.zeros(1, dtype=torch.int64, device=device)
+            N.check(N.lib().slg_rays_match_pinhole(_vp(rays), self.height, self.width, self.fx,
+                                                   self.fy, self.cx, self.cy, _vp(mism), _stream()))
+            self.table_is_pinhole = int(mism.item()) == 0
+            if keep_table or not self.table_is_pinhole:
+                self.rays = rays
+                self.ray_mode = N.RAYS_TABLE
+
+    def struct(self) -> N.Calib:
+        c = N.Calib()
+        c.rays = self.rays.data_ptr() if self.rays is not None else 0
+        c.ray_mode = self.ray_mode
+        c.fx, c.fy, c.cx, c.cy = self.fx, self.fy, self.cx, self.cy
+        for i in range(3):
+            c.oc[i] = float(self.oc[i]) if i < len(self.oc) else 0.0
+        c.col_planes = self.col_planes.data_ptr()
+        c.n_col_planes = self.col_planes.shape[0]
+        if self.row_planes is not None:
+            c.row_planes = self.row_planes.data_ptr()
+            c.n_row_planes = self.row_planes.shape[0]
+        return c
+
+
+# ----------------------------------------------------------------------------- engine
+@dataclass
+class DecodeConfig:
+    """Arguments of ``_gray_decode`` (server/processing.py:28-30) / ``gray_decode``."""
+    n_cols: int = 1920
+    n_rows: int = 1080
+    n_sets_col: int = 11
+    n_sets_row: int = 11
+    thresh_mode: str = "otsu"          # 'otsu' | 'manual' | 'percentile' (sl_system variant)
+    shadow_val: float = 40
+    contrast_val: float = 10
+    variant: str = "processing"        # 'processing' | 'slsystem'
+
+    def struct(self) -> N.DecodeParams:
+        if self.variant == "slsystem":
+            mode, var = N.THRESH_PERCENTILE, N.VARIANT_SLSYSTEM
+        else:
+            var = N.VARIANT_PROCESSING
+            mode = N.THRESH_OTSU if self.thresh_mode == "otsu" else N.THRESH_MANUAL
+        return N.DecodeParams(proj_cols=int(self.n_cols), proj_rows=int(self.n_rows),
+                              n_sets_col=int(self.n_sets_col), n_sets_row=int(self.n_sets_row),
+                              variant=var, thresh_mode=mode,
+                              shadow_val=weak_scalar(self.shadow_val),
+                              contrast_val=weak_scalar(self.contrast_val))
+
+
+class Cloud:
+    """Preallocated device output of one view (worst-case capacity)."""
+
+    def __init__(self, n_px: int, row_mode: int, xyz_f64: bool, device=None):
+        device = device or default_device()
+        self.capacity = n_px * (2 if row_mode == 2 else 1)
+        self.xyz = torch.empty((self.capacity, 3), device=device,
+                               dtype=torch.float64 if xyz_f64 else torch.float32)
+        self.bgr = torch.empty((self.capacity, 3), device=device, dtype=torch.uint8)
+        self.count = torch.zeros(1, device=device, dtype=torch.int64)
+        self.xyz_f64 = xyz_f64
+
+    def struct(self) -> N.Cloud:
+        return N.Cloud(xyz=self.xyz.data_ptr(), bgr=self.bgr.data_ptr(),
+                       count=self.count.data_ptr(), capacity=self.capacity)
+
+    def result(self):
+        n = int(self.count.item())
+        return self.xyz[:n], self.bgr[:n]
+
+
+class Reconstructor:
+    """Owns the workspace for one image size; every call is stream-ordered, no host sync."""
+
+    def __init__(self, height: int, width: int, device=None):
+        self.device = device or default_device()
+        self.height, self.width, self.n_px = int(height), int(width), int(height) * int(width)
+        nbytes = int(N.lib().slg_workspace_bytes(self.n_px))
+        self.workspace = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        N.check(N.lib().slg_workspace_init(_vp(self.workspace), nbytes, _stream()))
+
+    def _check_geometry(self, h, w):
+        if (h, w) != (self.height, self.width):
+            raise ValueError(f"engine built for {self.width}x{self.height}, got {w}x{h}")
+
+    def decode(self, frames: DeviceFrames, cfg: DecodeConfig, stream=None):
+        """Correspondence maps (col int32, row int32, mask uint8) of one capture."""
+        self._check_geometry(frames.height, frames.width)
+        cap, dp = frames.capture(), cfg.struct()
+        col = torch.empty(self.n_px, dtype=torch.int32, device=self.device)
+        row = torch.empty(self.n_px, dtype=torch.int32, device=self.device)
+        mask = torch.empty(self.n_px, dtype=torch.uint8, device=self.device)
+        s = _stream(stream)
+        L = N.lib()
+        N.check(L.slg_decode_stats(ctypes.byref(cap), ctypes.byref(dp), _vp(self.workspace), s))
+        N.check(L.slg_decode(ctypes.byref(cap), ctypes.byref(dp), _vp(self.workspace),
+                             _vp(col), _vp(row), _vp(mask), s))
+        return col, row, mask
+
+    def triangulate(self, col, row, mask, texture, calib: DeviceCalib, row_mode=1,
+                    epipolar_tol=2.0, xyz_f64=True, out: Cloud | None = None, stream=None):
+        """Cloud from device maps (``_reconstruct_point_cloud``)."""
+        self._check_geometry(calib.height, calib.width)
+        out = out or Cloud(self.n_px, row_mode, xyz_f64, self.device)
+        maps = N.Maps(col=col.data_ptr(), row=row.data_ptr() if row is not None else 0,
+                      mask=mask.data_ptr(), texture=texture.data_ptr(),
+                      height=self.height, width=self.width)
+        c, tp, o = calib.struct(), N.TriParams(int(row_mode), int(out.xyz_f64), float(epipolar_tol)), out.struct()
+        N.check(N.lib().slg_triangulate(ctypes.byref(maps), ctypes.byref(c), ctypes.byref(tp),
+                                        _vp(self.workspace), ctypes.byref(o), _stream(stream)))
+        return out
+
+    def reconstruct(self, frames: DeviceFrames, cfg: DecodeConfig, calib: DeviceCalib, row_mode=1,
+                    epipolar_tol=2.0, xyz_f64=True, out: Cloud | None = None, stream=None):
+        """Fused decode + triangulate of one view (maps stay on chip)."""
+        self._check_geometry(frames.height, frames.width)
+        self._check_geometry(calib.height, calib.width)
+        out = out or Cloud(self.n_px, row_mode, xyz_f64, self.device)
+        cap, dp, c = frames.capture(), cfg.struct(), calib.struct()
+        tp, o = N.TriParams(int(row_mode), int(out.xyz_f64), float(epipolar_tol)), out.struct()
+        N.check(N.lib().slg_reconstruct(ctypes.byref(cap), ctypes.byref(dp), ctypes.byref(c),
+                                        ctypes.byref(tp), _vp(self.workspace), ctypes.byref(o),
+                                        _stream(stream)))
+        return out
+
+    def thresholds(self):
+        """(shadow, contrast) float thresholds of the last stats pass (workspace header)."""
+        hdr = self.workspace[:8192].cpu().numpy()
+        off = 3 * 256 * 4 + 4 * 4 + 4 * 4
+        return tuple(np.frombuffer(hdr[off: off + 16].tobytes(), dtype=np.float64))
+
+    def error_flags(self) -> int:
+        hdr = self.workspace[:8192].cpu().numpy()
+        return int(np.frombuffer(hdr[3 * 256 * 4 + 12: 3 * 256 * 4 + 16].tobytes(), np.uint32)[0])

@@ -1,0 +1,88 @@
+"""Capture discovery and frame ingest (host side of the hot path).
+
+* Discovery keeps the reference's orders: ``ProcessingLogic._gray_decode`` globs ``*.bmp``
+  first, then ``*.png`` (``server/processing.py:49-54``); ``SLSystem.generate_cloud`` globs
+  ``*.png`` first, then ``*.bmp`` (``server/sl_system.py:518-520``); both ``sorted``.
+* ``imread_gray`` / ``imread_bgr`` stand in for ``cv2.imread(path, 0)`` / ``cv2.imread(path)``
+  (OpenCV is not in the image).  8-bit grayscale files — what the reference's capture writes
+  and what every test uses — decode identically (identity).  Colour files are converted with
+  libpng's ``rgb_to_gray`` fixed-point weights for PNG and OpenCV's ``BGR2GRAY`` weights for
+  BMP: that arithmetic is restated from the libraries' published formulas and is parity
+  unpinned (no OpenCV here to check against).  Decoding runs on a host thread pool.
+"""
+from __future__ import annotations
+
+import glob
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+
+def discover(source, order=("bmp", "png")):
+    """File list of a capture folder (or the list itself), in the reference's order."""
+    if isinstance(source, (list, tuple)):
+        return list(source)
+    for ext in order:
+        files = sorted(glob.glob(os.path.join(source, f"*.{ext}")))
+        if files:
+            return files
+    return []
+
+
+def _open(path):
+    from PIL import Image
+    try:
+        im = Image.open(path)
+        im.load()
+        return im
+    except (OSError, ValueError):
+        return None
+
+
+def _to_gray(im, path) -> np.ndarray:
+    a = np.asarray(im)
+    if a.dtype == np.uint16:
+        a = (a >> 8).astype(np.uint8)
+    if a.ndim == 2:
+        return np.ascontiguousarray(a, dtype=np.uint8)
+    rgb = a[..., :3].astype(np.uint32)
+    r, g, b = rgb[..., 0], rgb[..., 1], rgb[..., 2]
+    if str(path).lower().endswith(".bmp"):
+        # OpenCV icvCvt_BGR2Gray_8u_C3C1R: (b*1868 + g*9617 + r*4899 + 8192) >> 14
+        y = (b * 1868 + g * 9617 + r * 4899 + 8192) >> 14
+    else:
+        # libpng png_set_rgb_to_gray(…, 0.299, 0.587) 15-bit fixed point, 8-bit path
+        y = (r * 9797 + g * 19234 + b * 3737 + 16384) >> 15
+    return y.astype(np.uint8)
+
+
+def imread_gray(path) -> np.ndarray:
+    """``cv2.imread(path, 0)``; raises like ``None.astype`` would for unreadable files."""
+    im = _open(path)
+    if im is None:
+        raise AttributeError("'NoneType' object has no attribute 'astype'")
+    return _to_gray(im, path)
+
+
+def imread_bgr(path) -> np.ndarray:
+    """``cv2.imread(path)``: HxWx3 BGR uint8 (grayscale replicated)."""
+    im = _open(path)
+    if im is None:
+        raise AttributeError("'NoneType' object has no attribute 'reshape'")
+    a = np.asarray(im)
+    if a.dtype == np.uint16:
+        a = (a >> 8).astype(np.uint8)
+    if a.ndim == 2:
+        return np.repeat(a[..., None], 3, axis=-1).astype(np.uint8)
+    return np.ascontiguousarray(a[..., 2::-1][..., :3], dtype=np.uint8)
+
+
+def load_frames(files, indices=None, workers: int = 8):
+    """Decode the given frames (grayscale) on a thread pool; returns a list of arrays."""
+    idx = range(len(files)) if indices is None else indices
+    paths = [files[i] for i in idx]
+    if len(paths) <= 1:
+        return [imread_gray(p) for p in paths]
+    with ThreadPoolExecutor(max_workers=min(workers, len(paths))) as ex:
+        return list(ex.map(imread_gray, paths))

@@ -1,0 +1,215 @@
+"""Drop-in for the hot path of ``server/processing.py`` (class ``ProcessingLogic``).
+
+Same names, signatures, return types and error behaviour as the reference
+(``server/processing.py:27-334``); the arithmetic runs in the HIP kernels of ``libslgpu.so``.
+Only the reconstruction path is provided — the Open3D post-processing methods of the
+reference class (``remove_background`` ... ``mesh_360``, processing.py:336-860) are out of
+scope.
+"""
+from __future__ import annotations
+
+import glob
+import os
+
+import numpy as np
+import torch
+
+from . import engine as E
+from . import frames as FR
+from . import ply as PLY
+
+_ENGINES: dict = {}
+_CALIBS: dict = {}
+
+
+def _engine(h, w):
+    key = (h, w, torch.cuda.current_device())
+    if key not in _ENGINES:
+        _ENGINES[key] = E.Reconstructor(h, w)
+    return _ENGINES[key]
+
+
+def _device_calib(calib, h, w):
+    """Cache device tables per (calib dict object, geometry)."""
+    key = (id(calib), h, w)
+    hit = _CALIBS.get(key)
+    if hit is not None and hit[0] is calib:
+        return hit[1]
+    dc = E.DeviceCalib(calib, h, w)
+    _CALIBS[key] = (calib, dc)
+    return dc
+
+
+def _needed_frames(n_files, cfg: E.DecodeConfig):
+    """Frame indices the reference reads (processing.py:59-60,88-105)."""
+    Bc, Br = E.n_bits(cfg.n_cols), E.n_bits(cfg.n_rows)
+    need = [0, 1]
+    nc = max(1, min(int(cfg.n_sets_col), Bc))
+    nr = max(1, min(int(cfg.n_sets_row), Br))
+    idx = 2
+    for max_bits, n_use in ((Bc, nc), (Br, nr)):
+        for b in range(max_bits):
+            if idx + 1 < n_files and b < n_use:
+                need += [idx, idx + 1]
+            idx += 2
+    return need
+
+
+def load_capture(source, cfg: E.DecodeConfig, order=("bmp", "png")):
+    """Discover, decode (host thread pool) and upload one capture: ``(DeviceFrames, texture)``."""
+    files = FR.discover(source, order)
+    if len(files) < 4:
+        raise ValueError(f"Not enough images (got {len(files)}, need at least 4).")
+    need = _needed_frames(len(files), cfg) if cfg.variant == "processing" else list(range(len(files)))
+    imgs = FR.load_frames(files, need)
+    stack = [None] * len(files)
+    for i, im in zip(need, imgs):
+        stack[i] = im
+    texture = FR.imread_bgr(files[0])
+    return E.DeviceFrames(stack, texture), texture
+
+
+class ProcessingLogic:
+    """Reconstruction half of the reference's ``ProcessingLogic`` (processing.py:12-334)."""
+
+    # --- Multi PLY Processing Functions ---
+    @staticmethod
+    def _gray_decode(source, n_cols=1920, n_rows=1080,
+                     n_sets_col=11, n_sets_row=11,
+                     thresh_mode='otsu', shadow_val=40, contrast_val=10):
+        """Decode Gray-code images (server/processing.py:28-124).
+
+        ``source``: folder path or sorted file list, as in the reference; additionally a
+        ``DeviceFrames`` or a uint8 ``[F, H, W]`` array/tensor already in memory.
+        Returns ``(col int32[H,W], row int32[H,W], mask bool[H,W], texture uint8[H,W,3])``.
+        """
+        cfg = E.DecodeConfig(n_cols, n_rows, n_sets_col, n_sets_row, thresh_mode, shadow_val,
+                             contrast_val, "processing")
+        if isinstance(source, E.DeviceFrames):
+            dev = source
+            texture = source.texture.reshape(dev.height, dev.width, 3).cpu().numpy()
+        elif isinstance(source, (np.ndarray, torch.Tensor)) and source.ndim == 3:
+            dev = E.DeviceFrames(source)
+            texture = dev.texture.reshape(dev.height, dev.width, 3).cpu().numpy()
+        else:
+            dev, texture = load_capture(source, cfg)
+        eng = _engine(dev.height, dev.width)
+        col, row, mask = eng.decode(dev, cfg)
+        shape = (dev.height, dev.width)
+        return (col.reshape(shape).cpu().numpy(), row.reshape(shape).cpu().numpy(),
+                mask.reshape(shape).cpu().numpy().astype(bool), texture)
+
+    @staticmethod
+    def _reconstruct_point_cloud(col_map, row_map, mask, texture, calib,
+                                 row_mode=1, epipolar_tol=2.0):
+        """Ray-plane triangulation (server/processing.py:127-234).
+
+        Returns ``(P float64[N,3], C uint8[N,3] BGR)``; ``None`` for a ``row_mode`` other than
+        0/1/2 (the reference falls through its if-chain).
+        """
+        if row_mode not in (0, 1, 2):
+            return None
+        h, w = np.asarray(col_map).shape
+        eng = _engine(h, w)
+        dev = eng.device
+
+        def up(a, dt):
+            t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a, dtype=dt))
+            return t.reshape(-1).to(device=dev, dtype=torch.int32 if dt == np.int32 else torch.uint8)
+
+        col = up(col_map, np.int32)
+        row = up(row_map, np.int32) if row_mode != 0 else None
+        m = up(np.asarray(mask).astype(np.uint8) if not isinstance(mask, torch.Tensor) else mask, np.uint8)
+        tex = up(np.asarray(texture).reshape(-1, 3) if not isinstance(texture, torch.Tensor) else texture, np.uint8)
+        dc = _device_calib(calib, h, w)
+        out = eng.triangulate(col, row, m, tex, dc, row_mode, epipolar_tol, xyz_f64=True)
+        P, C = out.result()
+        return P.cpu().numpy(), C.cpu().numpy()
+
+    @staticmethod
+    def _save_ply(points, colors, filename):
+        """ASCII PLY, byte-identical to server/processing.py:236-248."""
+        PLY.write_ascii(filename, points, colors)
+
+    @staticmethod
+    def process_multi_ply(calib_path, target_path, mode, log_callback=None,
+                          n_sets_col=11, n_sets_row=11,
+                          row_mode=1, epipolar_tol=2.0,
+                          thresh_mode='otsu', shadow_val=40, contrast_val=10,
+                          file_list=None, out_path_override=None):
+        """Process structured-light images -> .ply point cloud (server/processing.py:251-334).
+
+        Each view runs the fused decode+triangulate kernel (maps never leave the chip)."""
+        def log(msg):
+            if log_callback: log_callback(msg)
+            else: print(msg)
+
+        log("Loading Calibration Data...")
+        import scipy.io
+        data = scipy.io.loadmat(calib_path)
+        calib_data = {
+            "Nc": data["Nc"], "Oc": data["Oc"],
+            "wPlaneCol": data["wPlaneCol"], "wPlaneRow": data["wPlaneRow"],
+            "cam_K": data["cam_K"]
+        }
+        cfg = E.DecodeConfig(1920, 1080, n_sets_col, n_sets_row, thresh_mode, shadow_val,
+                             contrast_val, "processing")
+
+        def _process_source(source, out_path, label):
+            log(f"  -> Decoding {label}  "
+                f"[col-sets={n_sets_col}  row-sets={n_sets_row}]...")
+            dev, _ = load_capture(source, cfg)
+            log("  -> Reconstructing 3D points...")
+            points, colors = reconstruct_view(dev, cfg, calib_data, row_mode, epipolar_tol)
+            log(f"  -> Saving {len(points)} points...")
+            ProcessingLogic._save_ply(points, colors, out_path)
+            log(f"  ✔ Saved: {os.path.basename(out_path)}\n")
+
+        if mode == "files":
+            if not file_list:
+                raise ValueError("mode='files' requires a non-empty file_list.")
+            if not out_path_override:
+                raise ValueError("mode='files' requires out_path_override.")
+            _process_source(file_list, out_path_override,
+                            f"{len(file_list)} selected files")
+
+        elif mode == "single":
+            ply_name = os.path.basename(target_path) + ".ply"
+            out_path = os.path.join(target_path, ply_name)
+            _process_source(target_path, out_path,
+                            f"folder '{os.path.basename(target_path)}'")
+
+        else:  # batch
+            subfolders = [f.path for f in os.scandir(target_path) if f.is_dir()]
+            log(f"Found {len(subfolders)} subfolders to process.")
+
+            success_count = 0
+            for folder in subfolders:
+                has_imgs = (glob.glob(os.path.join(folder, "*.bmp")) or
+                            glob.glob(os.path.join(folder, "*.png")))
+                if has_imgs:
+                    try:
+                        ply_name = os.path.basename(folder) + ".ply"
+                        out_path = os.path.join(folder, ply_name)
+                        _process_source(folder, out_path,
+                                        f"folder '{os.path.basename(folder)}'")
+                        success_count += 1
+                    except Exception as e:
+                        log(f"  ❌ Error in {os.path.basename(folder)}: {e}\n")
+                else:
+                    log(f"  Skipping {os.path.basename(folder)} (No images found).")
+
+            log(f"=== Batch Complete: {success_count}/{len(subfolders)} succeeded ===")
+
+
+def reconstruct_view(dev: E.DeviceFrames, cfg: E.DecodeConfig, calib: dict, row_mode=1,
+                     epipolar_tol=2.0, xyz_f64=True):
+    """Fused decode + triangulate of one in-HBM capture -> host ``(P, C)`` like the reference
+    pair ``_gray_decode`` + ``_reconstruct_point_cloud``."""
+    if row_mode not in (0, 1, 2):
+        return None
+    eng = _engine(dev.height, dev.width)
+    dc = _device_calib(calib, dev.height, dev.width)
+    out = eng.reconstruct(dev, cfg, dc, row_mode, epipolar_tol, xyz_f64=xyz_f64)
+    P, C = out.result()
+    return P.cpu().numpy(), C.cpu().numpy()

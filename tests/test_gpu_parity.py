@@ -1,0 +1,275 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden vectors and the
+oracle.  Integer/byte outputs (maps, mask, colours, order, counts) must be bit-exact; XYZ
+must be bit-exact in the float64 mode and within 1e-4 relative (north star) in float32 mode.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import decode_kwargs, golden_cases, load_calibs, load_case
+from oracle import sl_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+XYZ32_RTOL = 1e-4     # BASELINE.json north_star: XYZ within 1e-4 relative (fp32 vs float64)
+
+
+@pytest.fixture(scope="module")
+def mods():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a ROCm device")
+    from structured_light_for_3d_model_replication_amd import engine as E, processing as PR, _native as N
+    N.lib()
+    return E, PR, N
+
+
+def _cfg(E, p):
+    if p["variant"] == "slsystem":
+        return E.DecodeConfig(1920, 1080, variant="slsystem")
+    kw = decode_kwargs(p)
+    return E.DecodeConfig(kw.get("n_cols", 1920), kw.get("n_rows", 1080), kw.get("n_sets_col", 11),
+                          kw.get("n_sets_row", 11), kw.get("thresh_mode", "otsu"),
+                          kw.get("shadow_val", 40), kw.get("contrast_val", 10))
+
+
+def _xyz32_close(got, want):
+    got = np.asarray(got, np.float64)
+    scale = np.maximum(np.abs(want), 1e-3)
+    assert np.all(np.abs(got - want) <= XYZ32_RTOL * scale)
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_decode_maps_bit_exact(name, mods):
+    E, PR, N = mods
+    z = load_case(name)
+    dev = E.DeviceFrames(list(z["frames"]), z["texture"])
+    eng = E.Reconstructor(dev.height, dev.width)
+    cfg = _cfg(E, z["params"])
+    if "error" in z:
+        with pytest.raises(IndexError):
+            eng.decode(dev, cfg)
+        return
+    col, row, mask = eng.decode(dev, cfg)
+    shape = (dev.height, dev.width)
+    assert np.array_equal(col.reshape(shape).cpu().numpy(), z["col"])
+    assert np.array_equal(row.reshape(shape).cpu().numpy(), z["row"])
+    assert np.array_equal(mask.reshape(shape).cpu().numpy().astype(bool), z["mask"])
+
+
+@pytest.mark.parametrize("name", golden_cases())
+@pytest.mark.parametrize("fused", [False, True])
+def test_cloud_bit_exact_f64(name, fused, mods):
+    E, PR, N = mods
+    z = load_case(name)
+    if "error" in z:
+        pytest.skip("reference raises")
+    import torch
+    cal = load_calibs()[z["params"]["calib"]]
+    dev = E.DeviceFrames(list(z["frames"]), z["texture"])
+    eng = E.Reconstructor(dev.height, dev.width)
+    dc = E.DeviceCalib(cal, dev.height, dev.width)
+    cfg = _cfg(E, z["params"])
+    for rm in (0, 1, 2):
+        if f"P{rm}" not in z:
+            continue
+        if fused:
+            out = eng.reconstruct(dev, cfg, dc, row_mode=rm, xyz_f64=True)
+        else:
+            t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).reshape(-1).astype(dt)).cuda()
+            out = eng.triangulate(t(z["col"], np.int32), t(z["row"], np.int32),
+                                  t(z["mask"], np.uint8), dev.texture, dc, row_mode=rm, xyz_f64=True)
+        P, C = out.result()
+        P, C = P.cpu().numpy(), C.cpu().numpy()
+        assert P.shape == z[f"P{rm}"].shape, (rm, P.shape, z[f"P{rm}"].shape)
+        assert np.array_equal(P, z[f"P{rm}"]), f"row_mode {rm}: max |d| {np.abs(P - z[f'P{rm}']).max()}"
+        assert np.array_equal(C, z[f"C{rm}"]), f"row_mode {rm} colours"
+        assert eng.error_flags() == 0
+
+
+@pytest.mark.parametrize("name", ["proc_otsu_full", "proc_c2style", "proc_odd_geometry", "sl_full"])
+def test_cloud_f32_within_tolerance(name, mods):
+    E, PR, N = mods
+    z = load_case(name)
+    cal = load_calibs()[z["params"]["calib"]]
+    dev = E.DeviceFrames(list(z["frames"]), z["texture"])
+    eng = E.Reconstructor(dev.height, dev.width)
+    dc = E.DeviceCalib(cal, dev.height, dev.width)
+    for rm in (0, 1, 2):
+        if f"P{rm}" not in z:
+            continue
+        P, C = eng.reconstruct(dev, _cfg(E, z["params"]), dc, row_mode=rm, xyz_f64=False).result()
+        assert P.dtype.itemsize == 4
+        assert len(P) == len(z[f"P{rm}"])
+        _xyz32_close(P.cpu().numpy(), z[f"P{rm}"])
+        assert np.array_equal(C.cpu().numpy(), z[f"C{rm}"])
+
+
+def test_ray_table_paths_agree(mods):
+    """Nc gathered from the table == recomputed pinhole rays (bitwise), and the table is
+    detected as the pinhole one."""
+    E, PR, N = mods
+    z = load_case("proc_otsu_full")
+    cal = load_calibs()["rig"]
+    dev = E.DeviceFrames(list(z["frames"]), z["texture"])
+    eng = E.Reconstructor(dev.height, dev.width)
+    d_pin = E.DeviceCalib(cal, dev.height, dev.width)
+    d_tab = E.DeviceCalib(cal, dev.height, dev.width, keep_table=True)
+    assert d_pin.table_is_pinhole and d_pin.ray_mode == N.RAYS_PINHOLE
+    assert d_tab.ray_mode == N.RAYS_TABLE
+    cfg = _cfg(E, z["params"])
+    a = eng.reconstruct(dev, cfg, d_pin, 1).result()[0].cpu().numpy()
+    b = eng.reconstruct(dev, cfg, d_tab, 1).result()[0].cpu().numpy()
+    assert np.array_equal(a, b) and np.array_equal(a, z["P1"])
+    # a perturbed table is not the pinhole one and must be gathered
+    cal2 = dict(cal)
+    cal2["Nc"] = cal["Nc"].copy()
+    cal2["Nc"][0, 7] = np.nextafter(cal2["Nc"][0, 7], 1.0)
+    d2 = E.DeviceCalib(cal2, dev.height, dev.width)
+    assert not d2.table_is_pinhole and d2.ray_mode == N.RAYS_TABLE
+
+
+def test_dropin_file_api_matches_oracle(tmp_path, mods):
+    """ProcessingLogic._gray_decode on PNG files + _reconstruct_point_cloud, vs the oracle."""
+    E, PR, N = mods
+    from structured_light_for_3d_model_replication_amd import synth
+    rig = synth.default_rig(160, 120, 1920, 1080)
+    v = synth.render_view(rig, 33.0, seed=3)
+    files = synth.write_capture(v, str(tmp_path / "scan"))
+    cal = rig.tables()
+    col, row, mask, tex = PR.ProcessingLogic._gray_decode(str(tmp_path / "scan"), n_sets_col=10, n_sets_row=9)
+    oc, orow, om = O.decode_processing(list(v.frames), n_sets_col=10, n_sets_row=9)
+    assert np.array_equal(col, oc) and np.array_equal(row, orow) and np.array_equal(mask, om)
+    assert tex.shape == (120, 160, 3) and np.array_equal(tex[..., 0], v.frames[0])
+    for rm in (0, 1, 2):
+        P, C = PR.ProcessingLogic._reconstruct_point_cloud(col, row, mask, tex, cal, row_mode=rm)
+        Po, Co = O.reconstruct_processing(oc, orow, om, tex, cal, row_mode=rm)
+        assert P.dtype == np.float64 and np.array_equal(P, Po) and np.array_equal(C, Co)
+    assert PR.ProcessingLogic._reconstruct_point_cloud(col, row, mask, tex, cal, row_mode=3) is None
+    with pytest.raises(ValueError, match="Not enough images"):
+        PR.ProcessingLogic._gray_decode(files[:3])
+
+
+def test_process_multi_ply_batch(tmp_path, mods):
+    """Batch mode end to end: one PLY per view folder, byte-identical to the oracle's writer,
+    a bad folder is reported and skipped (processing.py:319-334)."""
+    E, PR, N = mods
+    from structured_light_for_3d_model_replication_amd import synth, calibration
+    rig = synth.default_rig(128, 96, 1920, 1080)
+    calibration.save_mat(str(tmp_path / "calib.mat"), rig.tables())
+    root = tmp_path / "obj"
+    views = {}
+    for k, ang in enumerate((0.0, 90.0)):
+        v = synth.render_view(rig, ang, seed=100 + k)
+        d = root / f"obj_{int(ang)}deg_scan"
+        synth.write_capture(v, str(d))
+        views[d] = v
+    bad = root / "bad_scan"
+    synth.write_capture(synth.render_view(rig, 0.0, seed=9, n_present=3), str(bad))
+    (root / "empty").mkdir()
+    logs = []
+    PR.ProcessingLogic.process_multi_ply(str(tmp_path / "calib.mat"), str(root), "batch",
+                                         log_callback=logs.append, n_sets_col=11, n_sets_row=10)
+    cal = calibration.load_mat(str(tmp_path / "calib.mat"))
+    for d, v in views.items():
+        c, r, m = O.decode_processing(list(v.frames), n_sets_col=11, n_sets_row=10)
+        tex = np.repeat(v.frames[0][..., None], 3, -1)
+        P, C = O.reconstruct_processing(c, r, m, tex, cal, row_mode=1)
+        assert (d / f"{d.name}.ply").read_bytes() == O.ply_bytes(P, C)
+    assert any("Error in bad_scan" in s and "Not enough images" in s for s in logs)
+    assert any("Skipping empty" in s for s in logs)
+    assert logs[-1].startswith("=== Batch Complete: 2/4 succeeded")
+
+
+def test_generate_cloud_legacy(tmp_path, mods, capsys):
+    E, PR, N = mods
+    from structured_light_for_3d_model_replication_amd import synth, calibration
+    from structured_light_for_3d_model_replication_amd.sl_system import SLSystem
+    rig = synth.default_rig(120, 80, 1920, 1080)
+    calibration.save_mat(str(tmp_path / "c.mat"), rig.tables())
+    v = synth.render_view(rig, 45.0, seed=4)
+    synth.write_capture(v, str(tmp_path / "scanA"))
+    SLSystem().generate_cloud(str(tmp_path / "scanA"), str(tmp_path / "c.mat"))
+    cal = calibration.load_mat(str(tmp_path / "c.mat"))
+    c, r, m = O.decode_slsystem(list(v.frames))
+    P, C = O.reconstruct_slsystem(c, r, m, np.repeat(v.frames[0][..., None], 3, -1), cal)
+    assert (tmp_path / "scanA" / "scanA.ply").read_bytes() == O.ply_bytes(P, C)
+    with pytest.raises(FileNotFoundError):
+        SLSystem().generate_cloud(str(tmp_path / "scanA"), str(tmp_path / "nope.mat"))
+
+
+@pytest.mark.parametrize("cam,proj,nsets,thresh", [
+    ((1920, 1080), (1920, 1080), (11, 10), "otsu"),      # C2
+    ((1280, 720), (1024, 1080), (10, 11), "otsu"),       # C1 geometry
+    ((1921, 1079), (1920, 1080), (8, 7), "manual"),      # ragged size, coarse codes
+])
+def test_full_size_parity(cam, proj, nsets, thresh, mods):
+    """BASELINE-size views: maps + f64 cloud equal the oracle, and decoded codes equal the
+    renderer's ground truth on lit, valid pixels (size-independent property)."""
+    E, PR, N = mods
+    from structured_light_for_3d_model_replication_amd import synth
+    rig = synth.default_rig(*cam, *proj)
+    n_present = 44 if proj == (1920, 1080) and nsets == (11, 10) else (22 if proj[0] == 1024 else None)
+    v = synth.render_view(rig, 10.0, seed=7, n_present=n_present)
+    cal = rig.tables()
+    kw = dict(n_cols=proj[0], n_rows=proj[1], n_sets_col=nsets[0], n_sets_row=nsets[1], thresh_mode=thresh)
+    dev = E.DeviceFrames(list(v.frames), v.texture)
+    eng = E.Reconstructor(dev.height, dev.width)
+    cfg = E.DecodeConfig(proj[0], proj[1], nsets[0], nsets[1], thresh)
+    col, row, mask = eng.decode(dev, cfg)
+    oc, orow, om = O.decode_processing(list(v.frames), **kw)
+    shape = (cam[1], cam[0])
+    col, row, mask = (col.reshape(shape).cpu().numpy(), row.reshape(shape).cpu().numpy(),
+                      mask.reshape(shape).cpu().numpy().astype(bool))
+    assert np.array_equal(col, oc) and np.array_equal(row, orow) and np.array_equal(mask, om)
+    if nsets == (11, 10) or nsets == (10, 11):
+        lit = v.lit & mask
+        assert np.array_equal(col[lit], v.proj_col[lit])
+    dc = E.DeviceCalib(cal, dev.height, dev.width)
+    rm = 1 if proj[0] == 1920 else 0
+    P, C = eng.reconstruct(dev, cfg, dc, rm, xyz_f64=True).result()
+    Po, Co = O.reconstruct_processing(oc, orow, om, v.texture, cal, row_mode=rm)
+    assert np.array_equal(P.cpu().numpy(), Po) and np.array_equal(C.cpu().numpy(), Co)
+    assert eng.error_flags() == 0
+
+
+def test_percentile_thresholds_large(mods):
+    """Legacy mask thresholds at 6000x4000 (n > 2**24: NumPy's float32 index rounding)."""
+    E, PR, N = mods
+    import torch
+    H, W = 4000, 6000
+    g = torch.Generator().manual_seed(1)
+    black = torch.randint(0, 30, (H, W), generator=g, dtype=torch.uint8)
+    white = torch.clamp(black.int() + torch.randint(0, 200, (H, W), generator=g), 0, 255).to(torch.uint8)
+    frames = torch.stack([white, black, white, black]).cuda()
+    dev = E.DeviceFrames(frames)
+    eng = E.Reconstructor(H, W)
+    col, row, mask = eng.decode(dev, E.DecodeConfig(variant="slsystem"))
+    want = O.mask_percentile(white.numpy(), black.numpy())
+    assert np.array_equal(mask.reshape(H, W).cpu().numpy().astype(bool), want)
+    ts, tc = eng.thresholds()
+    nf = np.percentile(black.numpy().astype(np.float32), 95)
+    assert np.float32(ts) == np.float32(nf * 1.5)
+
+
+def test_repeated_calls_and_streams(mods):
+    """Workspace re-arming across calls and concurrent streams with separate engines."""
+    E, PR, N = mods
+    import torch
+    z = load_case("proc_c2style")
+    cal = load_calibs()["rig"]
+    dev = E.DeviceFrames(list(z["frames"]), z["texture"])
+    engs = [E.Reconstructor(dev.height, dev.width) for _ in range(2)]
+    dc = E.DeviceCalib(cal, dev.height, dev.width)
+    cfg = _cfg(E, z["params"])
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = []
+    for it in range(6):
+        k = it % 2
+        with torch.cuda.stream(streams[k]):
+            outs.append(engs[k].reconstruct(dev, cfg, dc, 1, xyz_f64=True))
+    torch.cuda.synchronize()
+    for o in outs:
+        P, C = o.result()
+        assert np.array_equal(P.cpu().numpy(), z["P1"]) and np.array_equal(C.cpu().numpy(), z["C1"])

@@ -1,0 +1,155 @@
+"""CPU tests of the host side: ABI exports, frame discovery/ingest, PLY bytes, calibration
+tables, NEP-50 threshold semantics, decode planning and the synthetic renderer."""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, load_calibs
+from oracle import sl_oracle as O
+
+PKG = "structured_light_for_3d_model_replication_amd"
+
+
+def header_exports():
+    txt = open(os.path.join(ROOT, "include", "slgpu.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int32_t|int64_t|const char \*)\s*\*?(slg_\w+)\(", txt, re.M)))
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    from structured_light_for_3d_model_replication_amd import build
+    build.build_native()
+    code = (
+        "import ctypes, json, sys\n"
+        f"import {PKG}._native as N\n"
+        "L = N.lib()\n"
+        f"names = {header_exports()!r}\n"
+        "missing = [n for n in names if not hasattr(L, n)]\n"
+        "print(json.dumps({'missing': missing, 'v': L.slg_version(), 'hip': N.loaded_hip_runtimes(),"
+        " 'ws': L.slg_workspace_bytes(1920*1080)}))\n")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, check=True)
+    import json
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert len(header_exports()) >= 9
+    assert r["missing"] == [] and r["v"] == 1
+    assert len(r["hip"]) == 1, r["hip"]          # one HIP runtime (torch's) in the process
+    assert r["ws"] > 1920 * 1080 * 27
+
+
+def test_exports_match_ctypes_table():
+    from structured_light_for_3d_model_replication_amd import _native as N
+    assert sorted(N.EXPORTS) == header_exports()
+
+
+def test_ctypes_struct_layout_matches_header():
+    from structured_light_for_3d_model_replication_amd import _native as N
+    import ctypes
+    assert ctypes.sizeof(N.Capture) == 40
+    assert ctypes.sizeof(N.DecodeParams) == 40
+    assert ctypes.sizeof(N.Calib) == 8 + 8 + 32 + 24 + 16 + 16
+    assert ctypes.sizeof(N.TriParams) == 16
+    assert ctypes.sizeof(N.Cloud) == 32
+
+
+def test_discovery_orders(tmp_path):
+    from structured_light_for_3d_model_replication_amd import frames as FR
+    from PIL import Image
+    for name in ("02.png", "01.png", "01.bmp", "02.bmp"):
+        Image.fromarray(np.zeros((4, 4), np.uint8)).save(tmp_path / name)
+    proc = FR.discover(str(tmp_path))                        # processing.py:52-54: bmp first
+    sl = FR.discover(str(tmp_path), order=("png", "bmp"))    # sl_system.py:518-520: png first
+    assert [os.path.basename(p) for p in proc] == ["01.bmp", "02.bmp"]
+    assert [os.path.basename(p) for p in sl] == ["01.png", "02.png"]
+    assert FR.discover(["b", "a"]) == ["b", "a"]              # lists are used as given
+
+
+def test_gray_png_bmp_are_identity(tmp_path):
+    from structured_light_for_3d_model_replication_amd import frames as FR
+    from PIL import Image
+    a = np.random.default_rng(0).integers(0, 256, (13, 17)).astype(np.uint8)
+    for ext in ("png", "bmp"):
+        p = str(tmp_path / f"x.{ext}")
+        Image.fromarray(a, mode="L").save(p)
+        assert np.array_equal(FR.imread_gray(p), a)
+        bgr = FR.imread_bgr(p)
+        assert bgr.shape == (13, 17, 3) and np.array_equal(bgr[..., 1], a)
+    with pytest.raises(AttributeError):
+        FR.imread_gray(str(tmp_path / "missing.png"))
+
+
+def test_needed_frames_matches_reference_reads():
+    from structured_light_for_3d_model_replication_amd import processing as PR, engine as E
+    cfg = E.DecodeConfig(1920, 1080, 3, 2)
+    need = PR._needed_frames(46, cfg)
+    assert need == [0, 1, 2, 3, 4, 5, 6, 7, 24, 25, 26, 27]
+    need = PR._needed_frames(9, E.DecodeConfig(1920, 1080, 11, 11))
+    assert need == [0, 1, 2, 3, 4, 5, 6, 7]                  # pair (8, 9) missing
+
+
+def test_weak_scalar_follows_numpy_comparison():
+    from structured_light_for_3d_model_replication_amd.engine import weak_scalar
+    img = np.arange(256, dtype=np.float32)
+    for thr in (40, 30.5, 7.25, 16777217, 0.1, np.float64(30.1), np.float32(12.7), np.int64(9)):
+        want = img > thr
+        got = img.astype(np.float64) > weak_scalar(thr)
+        assert np.array_equal(want, got), thr
+
+
+def test_ply_bytes_match_reference_writer(tmp_path):
+    from structured_light_for_3d_model_replication_amd import ply
+    rng = np.random.default_rng(3)
+    P = rng.normal(0, 300, (500, 3))
+    P[:5] = [[-0.0, 0.0, 1e-9], [0.00005, 0.00015, -0.00005], [1.23445, 2.5, -2.5],
+             [1e6, -1e6, 123.45675], [0.12345, 0.98765, 5e-5]]
+    C = rng.integers(0, 256, (500, 3)).astype(np.uint8)
+    f = tmp_path / "a.ply"
+    ply.write_ascii(str(f), P, C)
+    assert f.read_bytes() == O.ply_bytes(P, C)
+    ply.write_ascii(str(f), np.zeros((0, 3)), np.zeros((0, 3), np.uint8))
+    assert f.read_bytes() == O.ply_bytes(np.zeros((0, 3)), np.zeros((0, 3), np.uint8))
+
+
+def test_calibration_tables_match_reference_calibrate_final():
+    from structured_light_for_3d_model_replication_amd import synth
+    ref = load_calibs()["rig"]
+    mine = synth.default_rig(96, 64, 1920, 1080).tables()
+    assert np.array_equal(mine["Nc"], ref["Nc"])           # bitwise: pinhole rays
+    for k in ("wPlaneCol", "wPlaneRow"):
+        assert mine[k].shape == ref[k].shape
+        np.testing.assert_allclose(mine[k], ref[k], rtol=0, atol=1e-12)
+    assert np.array_equal(mine["Oc"], ref["Oc"]) and np.array_equal(mine["cam_K"], ref["cam_K"])
+
+
+def test_mat_round_trip(tmp_path):
+    from structured_light_for_3d_model_replication_amd import calibration, synth
+    t = synth.default_rig(32, 16, 1920, 1080).tables()
+    p = str(tmp_path / "c.mat")
+    calibration.save_mat(p, t)
+    back = calibration.load_mat(p)
+    for k in calibration.CALIB_KEYS:
+        assert np.array_equal(back[k], t[k]), k
+
+
+def test_synth_is_deterministic_and_decodes_to_ground_truth():
+    from structured_light_for_3d_model_replication_amd import synth
+    rig = synth.default_rig(80, 60, 1920, 1080)
+    a = synth.render_view(rig, 15.0, seed=5)
+    b = synth.render_view(rig, 15.0, seed=5)
+    assert np.array_equal(a.frames, b.frames) and np.array_equal(a.texture, b.texture)
+    col, row, mask = O.decode_processing(list(a.frames), thresh_mode="otsu")
+    lit = a.lit & mask
+    assert lit.sum() > 0.3 * lit.size
+    assert np.array_equal(col[lit], a.proj_col[lit]) and np.array_equal(row[lit], a.proj_row[lit])
+
+
+def test_generate_patterns_is_gray_code():
+    from structured_light_for_3d_model_replication_amd.sl_system import SLSystem
+    P = SLSystem().generate_patterns()
+    assert len(P[0]) == 11 and len(P[1]) == 11
+    seq = O.gray_code_frames(1920, 1080, 1)
+    for b in range(11):
+        assert np.array_equal(P[0][b], seq[2 + 2 * b])
+        assert np.array_equal(P[1][b], seq[24 + 2 * b])
