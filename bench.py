@@ -1,0 +1,209 @@
+#!/usr/bin/env python
+"""Benchmark: decoded+triangulated Mpoints/s of the structured-light hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): one 1920x1080 view per step, 11 column + 10 row
+Gray-code bits with inverses + white/black (44 frames), Otsu mask, row_mode 1 (epipolar
+filter, tol 2.0), fp32 XYZ + BGR out.  A step = stats launch (histograms -> Otsu thresholds)
++ the fused decode/triangulate/compaction launch, inputs resident in HBM.  Steps rotate over a
+pool of distinct rendered turntable views (6 x 91 MB frame stacks > 256 MiB Infinity Cache) so
+frames stream from HBM; two HIP streams alternate so one view's Otsu overlaps the previous
+view's main kernel.  One process per GPU (torchrun); each rank renders its own views
+(weak scaling, no data-path collective); value = all ranks' points / max-over-ranks time.
+
+Prints ONE JSON line on stdout (rank 0).  Diagnostics go to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "decoded+triangulated Mpoints/sec (1 GPU & 8-GPU node); % of HBM roofline"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 measured copy)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(views, cal, seconds):
+    """Oracle (NumPy port of the reference path) on this host, one thread, frames in memory."""
+    import numpy as np
+    from oracle import sl_oracle as O
+    done, pts, t0 = 0, 0, time.perf_counter()
+    while True:
+        v = views[done % len(views)]
+        col, row, mask = O.decode_processing(list(v.frames), n_sets_col=11, n_sets_row=10)
+        P, _ = O.reconstruct_processing(col, row, mask, v.texture, cal, row_mode=1)
+        pts += len(P)
+        done += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(pts / dt / 1e6, 4), "unit": "Mpoints/s", "cores": 1, "kind": "port",
+            "sample": f"{done} C2 views (1920x1080, 11+10 bits, Otsu, row_mode 1), frames in "
+                      f"memory, oracle/sl_oracle.py NumPy restatement, 1 thread, {dt:.1f} s"}
+
+
+def load_traffic():
+    """HBM bytes per main_kernel launch from the committed rocprofv3 PMC summary, if any."""
+    p = os.path.join(ROOT, "profiles", "pmc_main_kernel.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--views", type=int, default=6)
+    ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--xyz", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from structured_light_for_3d_model_replication_amd import engine as E, synth, _native
+
+    W, H, PW, PH = 1920, 1080, 1920, 1080
+    rig = synth.default_rig(W, H, PW, PH)
+    cal = rig.tables()
+    t = time.perf_counter()
+    views = [synth.render_view(rig, view_deg=(rank * args.views + i) * 360.0 / (world * args.views),
+                               seed=1000 * rank + i, n_present=44) for i in range(args.views)]
+    log(f"[rank {rank}] rendered {len(views)} views in {time.perf_counter() - t:.1f}s")
+
+    cfg = E.DecodeConfig(PW, PH, 11, 10, "otsu")
+    row_mode, tol, f64 = 1, 2.0, args.xyz == "f64"
+    dframes = [E.DeviceFrames(list(v.frames), v.texture, device=dev) for v in views]
+    dcal = E.DeviceCalib(cal, H, W, device=dev)
+    S = max(1, args.streams)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
+    engs = [E.Reconstructor(H, W, device=dev) for _ in range(S)]
+    clouds = [E.Cloud(H * W, row_mode, f64, device=dev) for _ in range(S)]
+    structs = {(k, v): engs[k].launch_structs(dframes[v], cfg, dcal, clouds[k], row_mode, tol)
+               for k in range(S) for v in range(len(views))}
+
+    # points per view (also a sanity check of the GPU result against the pool)
+    pts = []
+    for v in range(len(views)):
+        engs[0].stats(dframes[v], cfg, stream=streams[0])
+        engs[0].decode_triangulate(dframes[v], cfg, dcal, clouds[0], row_mode, tol, stream=streams[0],
+                                   _structs=structs[(0, v)])
+        streams[0].synchronize()
+        pts.append(int(clouds[0].count.item()))
+    assert engs[0].error_flags() == 0
+
+    K, Wm = args.steps, args.warmup
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    total_pts = 0
+    bytes_alg = 0.0
+    out_b = 30 if f64 else 18            # 3 B texture read + 12|24 B XYZ + 3 B BGR per point
+    frame_b = (2 + 2 * (11 + 10)) * H * W
+
+    def step(i, timed_idx=None):
+        k, v = i % S, i % len(views)
+        s = streams[k]
+        engs[k].stats(dframes[v], cfg, stream=s)
+        if timed_idx is not None:
+            ev[timed_idx][0].record(s)
+        engs[k].decode_triangulate(dframes[v], cfg, dcal, clouds[k], row_mode, tol, stream=s,
+                                   _structs=structs[(k, v)])
+        if timed_idx is not None:
+            ev[timed_idx][1].record(s)
+        return v
+
+    for i in range(Wm):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(K):
+        v = step(Wm + j, j)
+        total_pts += pts[v]
+        bytes_alg += frame_b + out_b * pts[v]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev)
+    assert all(e.error_flags() == 0 for e in engs), "look-back timeout flag set"
+
+    stats = torch.tensor([dt, float(total_pts), kern_ms, bytes_alg], dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = stats[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        sums = stats[1:].clone()
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        dt_max = float(tmax.item())
+        all_pts, kern_sum, bytes_sum = (float(x) for x in sums.tolist())
+    else:
+        dt_max, all_pts, kern_sum, bytes_sum = dt, float(total_pts), kern_ms, bytes_alg
+
+    if rank == 0:
+        launches = K * world
+        kern_avg_s = kern_sum / launches / 1e3
+        achieved = bytes_sum / launches / kern_avg_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(),
+                "kernel": "main_kernel<1,0,1,0,1,1> (fused decode+triangulate+compaction)",
+                "kernel_avg_us": round(kern_avg_s * 1e6, 2),
+                "alg_bytes_per_launch": round(bytes_sum / launches)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(views, cal, args.cpu_seconds)
+        out = {
+            "metric": METRIC,
+            "value": round(all_pts / dt_max / 1e6, 2),
+            "unit": "Mpoints/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": Wm,
+            "ms_per_step": round(dt_max / K * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "C2: 1920x1080 view, 11 col + 10 row Gray bits + inverses + "
+                                   "white/black (44 frames), Otsu, row_mode 1 tol 2.0, XYZ "
+                                   f"{args.xyz} + BGR out",
+                       "views_per_rank": len(views), "points_per_view": int(np.mean(pts)),
+                       "streams": S, "decode": "u8 compares, int32 codes; triangulation f64",
+                       "parallelism": f"view-sharded x{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -19,6 +19,7 @@
  *   slg_reconstruct        <- decode + triangulate of one view as run by
  *                             process_multi_ply._process_source (server/processing.py:286-298)
  *                             without materialising the correspondence maps
+ *   slg_decode_triangulate <- the same without the stats launch (after slg_decode_stats)
  *   slg_rays_match_pinhole <- the `Nc.shape[1] == h*w` ray source test
  *                             (server/processing.py:143-156): tells whether the calibration's
  *                             Nc table equals the cam_K pinhole rays bit for bit, in which case
@@ -151,6 +152,12 @@ int32_t slg_triangulate(const slg_maps *maps, const slg_calib *calib, const slg_
 int32_t slg_reconstruct(const slg_capture *cap, const slg_decode_params *dp,
                         const slg_calib *calib, const slg_tri_params *tp, void *workspace,
                         const slg_cloud *out, void *stream);
+
+/* The fused decode+triangulate launch alone (slg_reconstruct minus the stats launch): call
+ * after slg_decode_stats on the same workspace and stream. */
+int32_t slg_decode_triangulate(const slg_capture *cap, const slg_decode_params *dp,
+                               const slg_calib *calib, const slg_tri_params *tp, void *workspace,
+                               const slg_cloud *out, void *stream);
 
 /* Count (into *mismatches, device int64) the Nc entries that differ bitwise from the cam_K
  * pinhole rays; 0 means SLG_RAYS_PINHOLE reproduces the table exactly. */

@@ -74,6 +74,9 @@ EXPORTS = {
     "slg_reconstruct": (c_i32, [ctypes.POINTER(Capture), ctypes.POINTER(DecodeParams),
                                 ctypes.POINTER(Calib), ctypes.POINTER(TriParams), c_vp,
                                 ctypes.POINTER(Cloud), c_vp]),
+    "slg_decode_triangulate": (c_i32, [ctypes.POINTER(Capture), ctypes.POINTER(DecodeParams),
+                                       ctypes.POINTER(Calib), ctypes.POINTER(TriParams), c_vp,
+                                       ctypes.POINTER(Cloud), c_vp]),
     "slg_rays_match_pinhole": (c_i32, [c_vp, c_i32, c_i32, c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_vp]),
 }
 

@@ -933,8 +933,9 @@ int32_t slg_triangulate(const slg_maps* maps, const slg_calib* calib, const slg_
   return launch_main(pick_tri<0, 0>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode), mp, tp, out, s);
 }
 
-int32_t slg_reconstruct(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,
-                        const slg_tri_params* tp, void* workspace, const slg_cloud* out, void* stream) {
+static int reconstruct_impl(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,
+                            const slg_tri_params* tp, void* workspace, const slg_cloud* out, void* stream,
+                            bool with_stats) {
   int rc = check_capture(cap);
   if (rc) return rc;
   if (!dp || !workspace || !cap->texture) return fail(SLG_ERR_INVALID, "NULL argument");
@@ -954,9 +955,21 @@ int32_t slg_reconstruct(const slg_capture* cap, const slg_decode_params* dp, con
   mp.col_first = pl.col_first; mp.col_pairs = pl.col_pairs; mp.col_pre = pl.col_pre; mp.col_post = pl.col_post;
   mp.row_first = pl.row_first; mp.row_pairs = pl.row_pairs; mp.row_pre = pl.row_pre; mp.row_post = pl.row_post;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  rc = stats_launch(cap->frames, cap->frames + cap->frame_stride, n_px, dp, workspace, s);
-  if (rc) return rc;
+  if (with_stats) {
+    rc = stats_launch(cap->frames, cap->frames + cap->frame_stride, n_px, dp, workspace, s);
+    if (rc) return rc;
+  }
   return launch_main(pick_tri<1, 0>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode), mp, tp, out, s);
+}
+
+int32_t slg_reconstruct(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,
+                        const slg_tri_params* tp, void* workspace, const slg_cloud* out, void* stream) {
+  return reconstruct_impl(cap, dp, calib, tp, workspace, out, stream, true);
+}
+
+int32_t slg_decode_triangulate(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,
+                               const slg_tri_params* tp, void* workspace, const slg_cloud* out, void* stream) {
+  return reconstruct_impl(cap, dp, calib, tp, workspace, out, stream, false);
 }
 
 int32_t slg_rays_match_pinhole(const double* rays, int32_t height, int32_t width, double fx, double fy, double cx,

@@ -253,6 +253,28 @@ class Reconstructor:
                                         _stream(stream)))
         return out
 
+    def stats(self, frames: DeviceFrames, cfg: DecodeConfig, stream=None):
+        """Mask-threshold pass alone (``slg_decode_stats``); arms the workspace."""
+        cap, dp = frames.capture(), cfg.struct()
+        N.check(N.lib().slg_decode_stats(ctypes.byref(cap), ctypes.byref(dp), _vp(self.workspace),
+                                         _stream(stream)))
+
+    def decode_triangulate(self, frames: DeviceFrames, cfg: DecodeConfig, calib: DeviceCalib,
+                           out: "Cloud", row_mode=1, epipolar_tol=2.0, stream=None,
+                           _structs=None):
+        """Fused main launch alone (``slg_decode_triangulate``), after :meth:`stats`."""
+        if _structs is None:
+            _structs = self.launch_structs(frames, cfg, calib, out, row_mode, epipolar_tol)
+        cap, dp, c, tp, o = _structs
+        N.check(N.lib().slg_decode_triangulate(ctypes.byref(cap), ctypes.byref(dp), ctypes.byref(c),
+                                               ctypes.byref(tp), _vp(self.workspace),
+                                               ctypes.byref(o), _stream(stream)))
+
+    def launch_structs(self, frames, cfg, calib, out, row_mode=1, epipolar_tol=2.0):
+        """Pre-built ctypes argument structs (lets a hot loop skip their construction)."""
+        return (frames.capture(), cfg.struct(), calib.struct(),
+                N.TriParams(int(row_mode), int(out.xyz_f64), float(epipolar_tol)), out.struct())
+
     def thresholds(self):
         """(shadow, contrast) float thresholds of the last stats pass (workspace header)."""
         hdr = self.workspace[:8192].cpu().numpy()
