@@ -26,6 +26,7 @@
 #include <string.h>
 #include <limits.h>
 #include <type_traits>
+#include <stdlib.h>
 
 #include "../../include/slgpu.h"
 
@@ -45,7 +46,7 @@ constexpr unsigned kMaxSpin = 1u << 22;
 
 // ------------------------------------------------------------------ workspace layout
 struct WsHeader {
-  uint32_t hist[3][256];   // 0: white, 1: clip(white-black,0,255), 2: black
+  uint32_t hist[3][256];   // otsu: 0 white, 1 clip(white-black,0,255); percentile: 0 black
   uint32_t max_diff_enc;   // max(white-black) + 256 (0 = none yet)
   uint32_t ticket;         // stats_kernel arrival counter
   uint32_t tile_counter;   // dynamic tile id for main_kernel
@@ -126,29 +127,93 @@ struct StatsParams {
   double contrast_val;
 };
 
-// OpenCV getThreshVal_Otsu_8u, sequential fp64 (see oracle/sl_oracle.py:otsu_from_hist).
-__device__ double otsu_from_hist(const uint32_t* h, int64_t total) {
-  const double scale = 1.0 / double(total);
-  double mu = 0.0;
-  for (int i = 0; i < 256; ++i) mu += double(i) * double(h[i]);
-  mu *= scale;
-  double mu1 = 0.0, q1 = 0.0, max_sigma = 0.0, max_val = 0.0;
+// OpenCV getThreshVal_Otsu_8u (see oracle/sl_oracle.py:otsu_from_hist) evaluated by one wave.
+// Bit-exact with the sequential fp64 loop: only order-independent pieces run in parallel.
+//  * mu = sum(i*h[i]) of exact integers (< 2^53) == OpenCV's sequential double sum;
+//  * q1 (running sum of p_i = h[i]*scale) and mu1 (mu1 = (mu1*q1_prev + i*p_i)/q1) keep their
+//    sequential fp order in lane 0, restricted to the contiguous range of non-skipped bins
+//    (before it mu1 stays exactly 0; after it no sigma is compared);
+//  * sigma per bin and the first-maximum argmax (strict '>' from 0) are lane-parallel.
+struct OtsuScratch {
+  double q[257];     // q[i] = q1 before bin i (q[0] = 0)
+  double pv[256];    // p_i
+  double m1[256];    // mu1 after bin i
+  uint8_t skip[256];
+};
+
+__device__ double otsu_wave(const uint32_t* h, int64_t n, OtsuScratch* sc) {
+  const int lane = threadIdx.x & 63;
+  const double scale = 1.0 / double(n);
   const double eps = double(__FLT_EPSILON__);
-  for (int i = 0; i < 256; ++i) {
-    const double p_i = double(h[i]) * scale;
-    mu1 *= q1;
-    q1 += p_i;
-    const double q2 = 1.0 - q1;
-    if (fmin(q1, q2) < eps || fmax(q1, q2) > 1.0 - eps) continue;
-    mu1 = (mu1 + double(i) * p_i) / q1;
-    const double mu2 = (mu - q1 * mu1) / q2;
-    const double sigma = q1 * q2 * (mu1 - mu2) * (mu1 - mu2);
-    if (sigma > max_sigma) {
-      max_sigma = sigma;
-      max_val = double(i);
+  uint64_t isum = 0;
+  for (int i = lane; i < 256; i += 64) {
+    sc->pv[i] = double(h[i]) * scale;
+    isum += uint64_t(i) * h[i];
+  }
+  isum = wave_sum(isum);
+  const double mu = double(isum) * scale;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (lane == 0) {
+    double acc = 0.0;
+    sc->q[0] = 0.0;
+#pragma unroll 16
+    for (int i = 0; i < 256; ++i) {
+      acc += sc->pv[i];
+      sc->q[i + 1] = acc;
     }
   }
-  return max_val;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  int first = 256, last = -1;
+  for (int i = lane; i < 256; i += 64) {
+    const double q1 = sc->q[i + 1], q2 = 1.0 - q1;
+    const bool sk = fmin(q1, q2) < eps || fmax(q1, q2) > 1.0 - eps;
+    sc->skip[i] = sk;
+    if (!sk) { first = min(first, i); last = max(last, i); }
+  }
+  first = wave_min_i(first);
+  last = -wave_min_i(-last);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (lane == 0) {
+    double mu1 = 0.0;
+    for (int i = first; i <= last; ++i) {
+      const double t = mu1 * sc->q[i];                                 // mu1 *= q1
+      mu1 = sc->skip[i] ? t : (t + double(i) * sc->pv[i]) / sc->q[i + 1];
+      sc->m1[i] = mu1;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  double best = 0.0;
+  int best_i = INT_MAX;
+  for (int i = lane; i < 256; i += 64) {
+    if (i < first || i > last || sc->skip[i]) continue;
+    const double q1 = sc->q[i + 1], q2 = 1.0 - q1, mu1 = sc->m1[i];
+    const double mu2 = (mu - q1 * mu1) / q2;
+    const double sigma = q1 * q2 * (mu1 - mu2) * (mu1 - mu2);
+    if (sigma > best) { best = sigma; best_i = i; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ob = __shfl_xor(best, o);
+    const int oi = __shfl_xor(best_i, o);
+    if (ob > best || (ob == best && oi < best_i)) { best = ob; best_i = oi; }
+  }
+  return best_i == INT_MAX ? 0.0 : double(best_i);
+}
+
+// smallest integer x in [lo, 256] with double(x) > thr (256 = none reachable)
+__device__ inline int int_threshold(double thr, int lo) {
+  if (!(thr == thr)) return 256;                 // NaN: comparison always false
+  if (thr < double(lo)) return lo;
+  if (thr >= 256.0) return 256;
+  return int(floor(thr)) + 1;
 }
 
 // k-th smallest value (0-based) from a 256-bin histogram.
@@ -179,10 +244,12 @@ __device__ float percentile95_from_hist(const uint32_t* h, int64_t n) {
 }
 
 __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
-  __shared__ uint32_t sh[3][256];
+  __shared__ uint32_t sh[4][2][256];        // per-wave sub-histograms (less LDS atomic contention)
+  __shared__ OtsuScratch s_otsu[2];
   __shared__ uint32_t s_maxd;
   __shared__ uint32_t s_last;
   const int tid = threadIdx.x;
+  const int wave = tid >> 6;
   WsHeader* ws = p.ws;
 
   // Arm the compaction state of the following main launch (ordered by the kernel boundary).
@@ -192,21 +259,18 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
 
   if (p.thresh_mode == SLG_THRESH_MANUAL) {
     if (blockIdx.x == 0 && tid < 2) {
-      // smallest integer x with double(x) > thr, over the reachable range
       const double thr = tid == 0 ? p.shadow_val : p.contrast_val;
-      const int lo = tid == 0 ? 0 : -255;
-      int m = 256;
-      for (int x = lo; x <= 256; ++x)
-        if (double(x) > thr) { m = x; break; }
+      const int m = int_threshold(thr, tid == 0 ? 0 : -255);
       if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
     }
     return;
   }
 
-  for (int i = tid; i < 3 * 256; i += kBlock) (&sh[0][0])[i] = 0;
+  for (int i = tid; i < 4 * 2 * 256; i += kBlock) (&sh[0][0][0])[i] = 0;
   if (tid == 0) s_maxd = 0;
   __syncthreads();
 
+  // hist slots: otsu -> [0] white, [1] clip(white-black); percentile -> [0] black
   const bool otsu = p.thresh_mode == SLG_THRESH_OTSU;
   uint32_t local_max = 0;
   const int64_t n_chunks = (p.n_px + kPx - 1) / kPx;
@@ -221,18 +285,18 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
       const int bv = ((k < 4 ? b.x : b.y) >> (8 * (k & 3))) & 0xff;
       const int d = wv - bv;
       if (otsu) {
-        atomicAdd(&sh[0][wv], 1u);
-        atomicAdd(&sh[1][d < 0 ? 0 : d], 1u);
+        atomicAdd(&sh[wave][0][wv], 1u);
+        atomicAdd(&sh[wave][1][d < 0 ? 0 : d], 1u);
       } else {
-        atomicAdd(&sh[2][bv], 1u);
+        atomicAdd(&sh[wave][0][bv], 1u);
         local_max = max(local_max, uint32_t(d + 256));
       }
     }
   }
   if (!otsu) atomicMax(&s_maxd, local_max);
   __syncthreads();
-  for (int i = tid; i < 3 * 256; i += kBlock) {
-    const uint32_t v = (&sh[0][0])[i];
+  for (int i = tid; i < 2 * 256; i += kBlock) {
+    const uint32_t v = (&sh[0][0][0])[i] + (&sh[1][0][0])[i] + (&sh[2][0][0])[i] + (&sh[3][0][0])[i];
     if (v) atomicAdd(&(&ws->hist[0][0])[i], v);
   }
   if (!otsu && tid == 0 && s_maxd) atomicMax(&ws->max_diff_enc, s_maxd);
@@ -255,33 +319,32 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  for (int i = tid; i < 3 * 256; i += kBlock)
-    (&sh[0][0])[i] = __hip_atomic_load(&(&ws->hist[0][0])[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t* hg = &sh[0][0][0];                 // reuse wave-0 slots for the global histograms
+  for (int i = tid; i < 2 * 256; i += kBlock)
+    hg[i] = __hip_atomic_load(&(&ws->hist[0][0])[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid == 0) s_maxd = __hip_atomic_load(&ws->max_diff_enc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  if (tid < 2) {
-    double thr;
-    int lo;
-    if (otsu) {
-      thr = otsu_from_hist(sh[tid], p.n_px);               // tid 0: white, 1: clip(w-b)
-      lo = tid == 0 ? 0 : -255;
-    } else {
-      if (tid == 0) {
-        const float nf = percentile95_from_hist(sh[2], p.n_px);
-        thr = double(nf * 1.5f);                           // noise_floor * 1.5 (float32)
-        lo = 0;
-      } else {
-        const float dr = float(int(s_maxd) - 256);         // np.max(contrast)
-        thr = double(dr * 0.05f);                          // dynamic_range * 0.05 (float32)
-        lo = -255;
+  if (otsu) {
+    if (wave < 2) {                            // wave 0: white, wave 1: clip(w-b); concurrently
+      const double thr = otsu_wave(hg + 256 * wave, p.n_px, &s_otsu[wave]);
+      if ((tid & 63) == 0) {
+        const int m = int_threshold(thr, wave == 0 ? 0 : -255);
+        if (wave == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
       }
     }
-    int m = 256;
-    for (int x = lo; x <= 256; ++x)
-      if (double(x) > thr) { m = x; break; }
+  } else if (tid < 2) {
+    double thr;
+    if (tid == 0) {
+      const float nf = percentile95_from_hist(hg, p.n_px);
+      thr = double(nf * 1.5f);                           // noise_floor * 1.5 (float32)
+    } else {
+      const float dr = float(int(s_maxd) - 256);         // np.max(contrast)
+      thr = double(dr * 0.05f);                          // dynamic_range * 0.05 (float32)
+    }
+    const int m = int_threshold(thr, tid == 0 ? 0 : -255);
     if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
   }
-  for (int i = tid; i < 3 * 256; i += kBlock) (&ws->hist[0][0])[i] = 0;
+  for (int i = tid; i < 2 * 256; i += kBlock) (&ws->hist[0][0])[i] = 0;
   if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
 }
 
@@ -323,6 +386,8 @@ struct MainParams {
   int64_t n_tiles;
   void* scratch_xyz;       // row_mode 2 row cloud
   uint8_t* scratch_bgr;
+  int32_t dbg;             // profiling ablations (env SLG_DBG, 0 in production): bit0 no look-back
+                           // wait, bit1 trivial triangulation, bit2 no output stores
 };
 
 template <int SRC_FRAMES>
@@ -485,6 +550,16 @@ __global__ __launch_bounds__(kBlock) void main_kernel(MainParams p) {
     }
     int v = int(px0 / p.width);
     int u = int(px0 - int64_t(v) * p.width);
+    if (p.dbg & 2) {
+      keep_c = valid;
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) { xc[k][0] = XT(col[k]); xc[k][1] = XT(row[k]); xc[k][2] = XT(u + k); }
+      if constexpr (ROW_MODE == 2) {
+        keep_r = valid;
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) { xr[k][0] = XT(row[k]); xr[k][1] = XT(col[k]); xr[k][2] = XT(v); }
+      }
+    } else
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
       if (valid & (1u << k)) {
@@ -579,7 +654,9 @@ __global__ __launch_bounds__(kBlock) void main_kernel(MainParams p) {
     uint64_t* st = p.states + int64_t(stream) * p.n_tiles;
     if (wave == 0) {
       uint64_t excl = 0;
-      if (tile == 0) {
+      if (p.dbg & 1) {
+        excl = uint64_t(tile) * kTilePx;                     // ablation: no inter-tile wait
+      } else if (tile == 0) {
         if (lane == 0) st_state(&st[0], kFlagInc | uint64_t(agg));
       } else {
         if (lane == 0) st_state(&st[tile], kFlagAgg | uint64_t(agg));
@@ -591,28 +668,33 @@ __global__ __launch_bounds__(kBlock) void main_kernel(MainParams p) {
             const int64_t s = j - (k * 64 + lane);
             vv[k] = s >= 0 ? ld_state(&st[s]) : kFlagInc;
           }
-          unsigned spins = 0;
+          // Wait only for entries newer than the nearest inclusive prefix; re-poll just the
+          // missing ones, with exponential back-off so waiting tiles do not flood the fabric.
+          unsigned spins = 0, nap = 1;
+          int pos;
           for (;;) {
+            int my_pos = INT_MAX;
+#pragma unroll
+            for (int k = kLookK - 1; k >= 0; --k)
+              if ((vv[k] >> 62) == 2) my_pos = k * 64 + lane;
+            pos = wave_min_i(my_pos);
             bool ready = true;
 #pragma unroll
-            for (int k = 0; k < kLookK; ++k) ready &= (vv[k] >> 62) != 0;
+            for (int k = 0; k < kLookK; ++k)
+              if (k * 64 + lane <= pos) ready &= (vv[k] >> 62) != 0;
             if (__all(ready)) break;
             if (++spins > kMaxSpin) {
               if (lane == 0) atomicOr(&p.ws->error, 1u);
               break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            for (unsigned z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(2);
+            nap = nap < 64 ? nap * 2 : 64;
 #pragma unroll
             for (int k = 0; k < kLookK; ++k) {
               const int64_t s = j - (k * 64 + lane);
-              if ((vv[k] >> 62) == 0 && s >= 0) vv[k] = ld_state(&st[s]);
+              if ((vv[k] >> 62) == 0 && s >= 0 && k * 64 + lane <= pos) vv[k] = ld_state(&st[s]);
             }
           }
-          int my_pos = INT_MAX;
-#pragma unroll
-          for (int k = kLookK - 1; k >= 0; --k)
-            if ((vv[k] >> 62) == 2) my_pos = k * 64 + lane;
-          const int pos = wave_min_i(my_pos);
           uint64_t sum = 0;
 #pragma unroll
           for (int k = 0; k < kLookK; ++k)
@@ -634,6 +716,7 @@ __global__ __launch_bounds__(kBlock) void main_kernel(MainParams p) {
     __syncthreads();
     const int64_t base = int64_t(s_excl);
 
+    if (p.dbg & 4) { __syncthreads(); continue; }
     // coalesced copy-out of the tile's compacted points
     XT* gx = reinterpret_cast<XT*>(stream == 0 ? p.xyz : p.scratch_xyz) + base * 3;
     for (int i = tid; i < agg * 3; i += kBlock) gx[i] = s_xyz[i];
@@ -782,7 +865,7 @@ int stats_launch(const uint8_t* white, const uint8_t* black, int64_t n_px, const
   sp.contrast_val = dp ? dp->contrast_val : 0.0;
   const int64_t chunks = (n_px + kPx - 1) / kPx;
   int64_t grid = (chunks + kBlock - 1) / kBlock;
-  if (grid > 1024) grid = 1024;
+  if (grid > 512) grid = 512;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(stats_kernel, dim3(unsigned(grid)), dim3(kBlock), 0, s, sp);
   return check_launch("stats_kernel");
@@ -838,8 +921,14 @@ int fill_out(MainParams& mp, const slg_cloud* out, const slg_tri_params* tp, int
   return SLG_OK;
 }
 
-int launch_main(MainFn fn, const MainParams& mp, const slg_tri_params* tp, const slg_cloud* out, hipStream_t s) {
+int debug_flags() {   // profiling ablations only; unset in production
+  const char* e = getenv("SLG_DBG");
+  return e ? atoi(e) : 0;
+}
+
+int launch_main(MainFn fn, MainParams mp, const slg_tri_params* tp, const slg_cloud* out, hipStream_t s) {
   if (!fn) return fail(SLG_ERR_INVALID, "no kernel for this configuration");
+  mp.dbg = debug_flags();
   hipLaunchKernelGGL(fn, dim3(unsigned(mp.n_tiles)), dim3(kBlock), 0, s, mp);
   int rc = check_launch("main_kernel");
   if (rc) return rc;

@@ -1,0 +1,108 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the view-sharded path: shard ranges,
+job-wide batch summary and the cloud gatherv used at the end of a job."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from structured_light_for_3d_model_replication_amd import distributed as D
+
+
+def test_shard_ranges_cover_views_exactly():
+    for n in (0, 1, 7, 36, 576):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for r in range(world):
+                lo, hi = D.shard_range(n, r, world)
+                seen += list(range(lo, hi))
+                assert hi - lo in (n // world, n // world + 1)
+            assert seen == list(range(n))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, tmp, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _body(rank, tmp, q)
+    except BaseException as e:  # report instead of hanging the parent on q.get
+        q.put((rank, [f"EXC {type(e).__name__}: {e}"]))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _body(rank, tmp, q):
+    if True:
+        # gatherv of ragged clouds
+        n = 5 + 3 * rank
+        xyz = torch.arange(n * 3, dtype=torch.float32).reshape(n, 3) + 1000 * rank
+        bgr = (torch.arange(n * 3, dtype=torch.int64).reshape(n, 3) % 251 + rank).to(torch.uint8)
+        got = D.gather_clouds(xyz, bgr, dst=0)
+        if rank == 0:
+            for r, (gx, gb) in enumerate(got):
+                m = 5 + 3 * r
+                assert torch.equal(gx, torch.arange(m * 3, dtype=torch.float32).reshape(m, 3) + 1000 * r)
+                assert torch.equal(gb, (torch.arange(m * 3).reshape(m, 3) % 251 + r).to(torch.uint8))
+        else:
+            assert got is None
+        # float64 clouds and an empty rank
+        xyz64 = torch.randn(0 if rank else 4, 3, dtype=torch.float64, generator=torch.Generator().manual_seed(1))
+        got = D.gather_clouds(xyz64, torch.zeros(xyz64.shape[0], 3, dtype=torch.uint8), dst=0)
+        if rank == 0:
+            assert got[0][0].shape == (4, 3) and got[1][0].shape == (0, 3)
+            assert torch.equal(got[0][0], xyz64)
+        # sharded batch with an injected per-view processor: per-folder error isolation and
+        # the job-wide summary line on rank 0
+        logs = []
+
+        def proc(folder, out_path):
+            if folder.endswith("bad"):
+                raise ValueError("Not enough images (got 3, need at least 4).")
+            with open(out_path, "w") as f:
+                f.write(str(rank))
+
+        D.process_batch_sharded("unused.mat", tmp, log_callback=logs.append, process_source=proc)
+        q.put((rank, logs))
+
+
+def test_gloo_world2_gather_and_sharded_batch(tmp_path):
+    names = ["v000", "v090", "v180", "bad", "v270"]
+    for n in names:
+        d = tmp_path / n
+        d.mkdir()
+        (d / "01.png").write_bytes(b"x")
+    (tmp_path / "empty").mkdir()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    assert not any(s.startswith("EXC") for logs in res.values() for s in logs), res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    folders = sorted(names + ["empty"])
+    lo, hi = D.shard_range(len(folders), 0, 2)
+    for i, f in enumerate(folders):
+        ply = tmp_path / f / f"{f}.ply"
+        if f in ("bad", "empty"):
+            assert not ply.exists()
+        else:
+            assert ply.read_text() == ("0" if lo <= i < hi else "1")
+    assert res[0][-1] == "=== Batch Complete: 4/6 succeeded ==="
+    assert not any("Batch Complete" in s for s in res[1])
+    assert any("Error in bad" in s for s in res[0] + res[1])

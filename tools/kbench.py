@@ -1,0 +1,102 @@
+#!/usr/bin/env python
+"""Per-kernel microbenchmark (one process, interleaved variants, HIP events on the launch
+stream).  Usage on the GPU box:  python tools/kbench.py [--iters 50] [--size 1920x1080]
+
+Reports, per variant, the median / min device time of:
+  stats      slg_decode_stats (histograms + Otsu / percentile)
+  main_rm{0,1,2}  slg_decode_triangulate (fused decode + triangulate + compaction)
+  decode     slg_decode (maps out)
+  tri_rm1    slg_triangulate (from maps)
+with frames rotated over a pool of views so they stream from HBM.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--size", default="1920x1080")
+    ap.add_argument("--views", type=int, default=6)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    from structured_light_for_3d_model_replication_amd import engine as E, synth
+
+    W, H = (int(x) for x in args.size.split("x"))
+    rig = synth.default_rig(W, H, 1920, 1080)
+    cal = rig.tables()
+    views = [synth.render_view(rig, 360.0 * i / args.views, seed=i, n_present=44) for i in range(args.views)]
+    dfr = [E.DeviceFrames(list(v.frames), v.texture) for v in views]
+    dcal = E.DeviceCalib(cal, H, W)
+    eng = E.Reconstructor(H, W)
+    cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
+    s = torch.cuda.current_stream()
+    clouds = {rm: E.Cloud(H * W, rm, False) for rm in (0, 1, 2)}
+    maps = [eng.decode(d, cfg) for d in dfr]
+    n_px = H * W
+
+    def timeit(fn, pre=None):
+        ts = []
+        for i in range(args.iters):
+            v = i % len(dfr)
+            if pre:
+                pre(v)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            fn(v)
+            b.record(s)
+            ts.append((a, b))
+        torch.cuda.synchronize()
+        us = [x.elapsed_time(y) * 1e3 for x, y in ts][3:]
+        return {"median_us": round(statistics.median(us), 2), "min_us": round(min(us), 2)}
+
+    res = {}
+    want = set(args.only.split(",")) if args.only else None
+
+    def run(name, fn, pre=None, alg_bytes=None):
+        if want and name not in want:
+            return
+        r = timeit(fn, pre)
+        if alg_bytes:
+            r["alg_GBps_at_median"] = round(alg_bytes / (r["median_us"] * 1e-6) / 1e9, 1)
+        res[name] = r
+        print(name, r, file=sys.stderr, flush=True)
+
+    run("stats", lambda v: eng.stats(dfr[v], cfg))
+    pts = {}
+    for rm in (0, 1, 2):
+        def f(v, rm=rm):
+            eng.decode_triangulate(dfr[v], cfg, dcal, clouds[rm], rm)
+        eng.stats(dfr[0], cfg)
+        f(0)
+        pts[rm] = int(clouds[rm].count.item())
+        frame_b = (2 + 2 * 11 + (2 * 10 if rm else 0)) * n_px
+        run(f"main_rm{rm}", f, pre=lambda v: eng.stats(dfr[v], cfg), alg_bytes=frame_b + 18 * pts[rm])
+    run("decode", lambda v: eng.decode(dfr[v], cfg), alg_bytes=(44 + 9) * n_px)
+    run("tri_rm1", lambda v: eng.triangulate(maps[v][0], maps[v][1], maps[v][2], dfr[v].texture, dcal, 1,
+                                             xyz_f64=False, out=clouds[1]),
+        alg_bytes=9 * n_px + 18 * pts[1])
+    for dbg in (1, 2, 4, 3, 7):
+        os.environ["SLG_DBG"] = str(dbg)
+        run(f"tri_rm1_dbg{dbg}", lambda v: eng.triangulate(maps[v][0], maps[v][1], maps[v][2], dfr[v].texture,
+                                                          dcal, 1, xyz_f64=False, out=clouds[1]))
+        run(f"main_rm1_dbg{dbg}", lambda v: eng.decode_triangulate(dfr[v], cfg, dcal, clouds[1], 1),
+            pre=lambda v: eng.stats(dfr[v], cfg))
+    os.environ.pop("SLG_DBG", None)
+    res["points"] = pts
+    res["error_flags"] = eng.error_flags()
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
