@@ -125,79 +125,70 @@ struct StatsParams {
   int32_t pad;
   double shadow_val;
   double contrast_val;
+  int32_t dbg;             // profiling ablation (SLG_DBG bit 4: skip the Otsu tail)
 };
 
 // OpenCV getThreshVal_Otsu_8u (see oracle/sl_oracle.py:otsu_from_hist) evaluated by one wave.
 // Bit-exact with the sequential fp64 loop: only order-independent pieces run in parallel.
 //  * mu = sum(i*h[i]) of exact integers (< 2^53) == OpenCV's sequential double sum;
-//  * q1 (running sum of p_i = h[i]*scale) and mu1 (mu1 = (mu1*q1_prev + i*p_i)/q1) keep their
-//    sequential fp order in lane 0, restricted to the contiguous range of non-skipped bins
-//    (before it mu1 stays exactly 0; after it no sigma is compared);
+//  * q1 (running sum of p_i = h[i]*scale) and mu1 (mu1 = (mu1*q1_prev + i*p_i)/q1) are one
+//    fused sequential chain on wave-uniform registers (v_readlane of the bin's p_i, results
+//    kept by the owning lane); bins that OpenCV skips cost no division, and the chain
+//    stops once q1 > 1-FLT_EPSILON (every later bin is skipped);
 //  * sigma per bin and the first-maximum argmax (strict '>' from 0) are lane-parallel.
-struct OtsuScratch {
-  double q[257];     // q[i] = q1 before bin i (q[0] = 0)
-  double pv[256];    // p_i
-  double m1[256];    // mu1 after bin i
-  uint8_t skip[256];
-};
+__device__ inline double readlane_f64(double v, int l) {
+  const uint64_t b = uint64_t(__double_as_longlong(v));
+  const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(b), l);
+  const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(b >> 32), l);
+  return __longlong_as_double((long long)((uint64_t(hi) << 32) | lo));
+}
 
-__device__ double otsu_wave(const uint32_t* h, int64_t n, OtsuScratch* sc) {
+__device__ double otsu_wave(const uint32_t* h, int64_t n) {
   const int lane = threadIdx.x & 63;
   const double scale = 1.0 / double(n);
   const double eps = double(__FLT_EPSILON__);
+  double pv[4], q1r[4], m1r[4];
+  uint32_t okr = 0;                                  // bit j: bin 4*lane+j not skipped
   uint64_t isum = 0;
-  for (int i = lane; i < 256; i += 64) {
-    sc->pv[i] = double(h[i]) * scale;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = 4 * lane + j;
+    pv[j] = double(h[i]) * scale;
     isum += uint64_t(i) * h[i];
+    q1r[j] = 0.0;
+    m1r[j] = 0.0;
   }
   isum = wave_sum(isum);
   const double mu = double(isum) * scale;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  if (lane == 0) {
-    double acc = 0.0;
-    sc->q[0] = 0.0;
-#pragma unroll 16
-    for (int i = 0; i < 256; ++i) {
-      acc += sc->pv[i];
-      sc->q[i + 1] = acc;
+  double q1 = 0.0, mu1 = 0.0;
+  for (int l = 0; l < 64; ++l) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double p_i = readlane_f64(pv[j], l);
+      mu1 *= q1;                                     // mu1 *= q1 (previous q1)
+      q1 += p_i;
+      const double q2 = 1.0 - q1;
+      const int skip = __builtin_amdgcn_readfirstlane(int(fmin(q1, q2) < eps || fmax(q1, q2) > 1.0 - eps));
+      if (!skip) {
+        mu1 = (mu1 + double(4 * l + j) * p_i) / q1;
+        if (lane == l) {                             // results back to the bin's lane
+          q1r[j] = q1;
+          m1r[j] = mu1;
+          okr |= 1u << j;
+        }
+      }
     }
+    if (__builtin_amdgcn_readfirstlane(int(q1 > 1.0 - eps))) break;   // all later bins skipped
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  int first = 256, last = -1;
-  for (int i = lane; i < 256; i += 64) {
-    const double q1 = sc->q[i + 1], q2 = 1.0 - q1;
-    const bool sk = fmin(q1, q2) < eps || fmax(q1, q2) > 1.0 - eps;
-    sc->skip[i] = sk;
-    if (!sk) { first = min(first, i); last = max(last, i); }
-  }
-  first = wave_min_i(first);
-  last = -wave_min_i(-last);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  if (lane == 0) {
-    double mu1 = 0.0;
-    for (int i = first; i <= last; ++i) {
-      const double t = mu1 * sc->q[i];                                 // mu1 *= q1
-      mu1 = sc->skip[i] ? t : (t + double(i) * sc->pv[i]) / sc->q[i + 1];
-      sc->m1[i] = mu1;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   double best = 0.0;
   int best_i = INT_MAX;
-  for (int i = lane; i < 256; i += 64) {
-    if (i < first || i > last || sc->skip[i]) continue;
-    const double q1 = sc->q[i + 1], q2 = 1.0 - q1, mu1 = sc->m1[i];
-    const double mu2 = (mu - q1 * mu1) / q2;
-    const double sigma = q1 * q2 * (mu1 - mu2) * (mu1 - mu2);
-    if (sigma > best) { best = sigma; best_i = i; }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!(okr & (1u << j))) continue;
+    const double q1j = q1r[j], q2 = 1.0 - q1j, mu1j = m1r[j];
+    const double mu2 = (mu - q1j * mu1j) / q2;
+    const double sigma = q1j * q2 * (mu1j - mu2) * (mu1j - mu2);
+    if (sigma > best) { best = sigma; best_i = 4 * lane + j; }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -245,7 +236,6 @@ __device__ float percentile95_from_hist(const uint32_t* h, int64_t n) {
 
 __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   __shared__ uint32_t sh[4][2][256];        // per-wave sub-histograms (less LDS atomic contention)
-  __shared__ OtsuScratch s_otsu[2];
   __shared__ uint32_t s_maxd;
   __shared__ uint32_t s_last;
   const int tid = threadIdx.x;
@@ -326,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   __syncthreads();
   if (otsu) {
     if (wave < 2) {                            // wave 0: white, wave 1: clip(w-b); concurrently
-      const double thr = otsu_wave(hg + 256 * wave, p.n_px, &s_otsu[wave]);
+      const double thr = (p.dbg & 16) ? 100.0 : otsu_wave(hg + 256 * wave, p.n_px);
       if ((tid & 63) == 0) {
         const int m = int_threshold(thr, wave == 0 ? 0 : -255);
         if (wave == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
@@ -739,6 +729,358 @@ __global__ __launch_bounds__(kBlock) void main_kernel(MainParams p) {
   }
 }
 
+// ------------------------------------------------------------------ main2: LDS-compacted triangulation
+// Exclusive prefix of `agg` over the tiles before `tile` (decoupled look-back; wave 0 calls it,
+// lane 0 publishes).  Waits only for entries newer than the nearest inclusive prefix and
+// re-polls just those, with exponential back-off.
+__device__ uint64_t lookback_prefix(uint64_t* st, int tile, int agg, int dbg, uint32_t* err) {
+  const int lane = threadIdx.x & 63;
+  uint64_t excl = 0;
+  if (dbg & 1) return uint64_t(tile) * kTilePx;               // ablation: no inter-tile wait
+  if (tile == 0) {
+    if (lane == 0) st_state(&st[0], kFlagInc | uint64_t(agg));
+    return 0;
+  }
+  if (lane == 0) st_state(&st[tile], kFlagAgg | uint64_t(agg));
+  int64_t j = tile - 1;
+  for (;;) {
+    uint64_t vv[kLookK];
+#pragma unroll
+    for (int k = 0; k < kLookK; ++k) {
+      const int64_t s = j - (k * 64 + lane);
+      vv[k] = s >= 0 ? ld_state(&st[s]) : kFlagInc;
+    }
+    unsigned spins = 0, nap = 1;
+    int pos;
+    for (;;) {
+      int my_pos = INT_MAX;
+#pragma unroll
+      for (int k = kLookK - 1; k >= 0; --k)
+        if ((vv[k] >> 62) == 2) my_pos = k * 64 + lane;
+      pos = wave_min_i(my_pos);
+      bool ready = true;
+#pragma unroll
+      for (int k = 0; k < kLookK; ++k)
+        if (k * 64 + lane <= pos) ready &= (vv[k] >> 62) != 0;
+      if (__all(ready)) break;
+      if (++spins > kMaxSpin) {
+        if (lane == 0) atomicOr(err, 1u);
+        break;
+      }
+      for (unsigned z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(2);
+      nap = nap < 64 ? nap * 2 : 64;
+#pragma unroll
+      for (int k = 0; k < kLookK; ++k) {
+        const int64_t s = j - (k * 64 + lane);
+        if ((vv[k] >> 62) == 0 && s >= 0 && k * 64 + lane <= pos) vv[k] = ld_state(&st[s]);
+      }
+    }
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kLookK; ++k)
+      if (k * 64 + lane <= pos) sum += vv[k] & kValMask;
+    excl += wave_sum(sum);
+    if (pos != INT_MAX) break;
+    j -= kLookK * 64;
+  }
+  if (lane == 0) st_state(&st[tile], kFlagInc | (excl + uint64_t(agg)));
+  return excl;
+}
+
+// Block-wide exclusive scan of one int per thread; returns (exclusive, total).
+__device__ inline int2 block_scan(int x, int* s_tot4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_tot4[wave] = incl;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    off += (w < wave) ? s_tot4[w] : 0;
+    tot += s_tot4[w];
+  }
+  __syncthreads();
+  return make_int2(off + incl - x, tot);
+}
+
+// Column/row code of all used pairs with every frame load of a batch in flight first.
+__device__ inline void decode_axis_mlp(const MainParams& p, int first, int pairs, int pre, int post,
+                                       int64_t px0, bool full, uint32_t (&acc)[4]) {
+  constexpr int G = 8;
+  acc[0] = acc[1] = acc[2] = acc[3] = 0u;
+  for (int b0 = 0; b0 < pairs; b0 += G) {
+    uint2 pv[G], iv[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (b0 + g < pairs) {
+        const uint8_t* fp = p.frames + int64_t(first + 2 * (b0 + g)) * p.stride;
+        if (full) {
+          pv[g] = *reinterpret_cast<const uint2*>(fp + px0);
+          iv[g] = *reinterpret_cast<const uint2*>(fp + p.stride + px0);
+        } else {
+          pv[g] = load8(fp, px0, p.n_px);
+          iv[g] = load8(fp + p.stride, px0, p.n_px);
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (b0 + g < pairs) {
+        const uint32_t m0 = gt_u8x4(pv[g].x, iv[g].x);
+        const uint32_t m1 = gt_u8x4(pv[g].y, iv[g].y);
+        acc[0] = (acc[0] << 1) | ((m0 >> 7) & 0x00010001u);
+        acc[1] = (acc[1] << 1) | ((m0 >> 15) & 0x00010001u);
+        acc[2] = (acc[2] << 1) | ((m1 >> 7) & 0x00010001u);
+        acc[3] = (acc[3] << 1) | ((m1 >> 15) & 0x00010001u);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = gray2bin_x2(acc[j] << pre) << post;
+}
+
+template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS>
+__global__ __launch_bounds__(kBlock) void main2_kernel(MainParams p) {
+  using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
+  constexpr int NS = ROW_MODE == 2 ? 2 : 1;
+  __shared__ uint32_t s_code[kTilePx];     // valid item m: col | row << 16
+  __shared__ uint16_t s_off[kTilePx];      // pixel offset inside the tile
+  __shared__ uint32_t s_tex[kTilePx];      // B | G << 8 | R << 16
+  __shared__ XT s_xyz[NS][kTilePx * 3];
+  __shared__ uint8_t s_keep[kTilePx];      // bit 0: column stream, bit 1: row stream
+  __shared__ uint16_t s_map[kTilePx];      // output slot -> item
+  __shared__ int s_tot4[4];
+  __shared__ int s_tile;
+  __shared__ uint64_t s_excl;
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  if (tid == 0) s_tile = (p.dbg & 8) ? int(blockIdx.x) : int(atomicAdd(&p.ws->tile_counter, 1u));
+  __syncthreads();
+  const int tile = s_tile;
+  const int64_t px0 = int64_t(tile) * kTilePx + int64_t(tid) * kPx;
+  const bool full = px0 + kPx <= p.n_px;
+
+  // ------------------------------------------------------------ phase A: decode 8 pixels
+  uint32_t valid = 0;
+  int col[kPx], row[kPx];
+  uint32_t tex[6] = {0, 0, 0, 0, 0, 0};
+  if (SRC_FRAMES) {
+    const int smin = p.ws->smin, cmin = p.ws->cmin;
+    const uint2 w = load8(p.frames, px0, p.n_px);
+    const uint2 bl = load8(p.frames + p.stride, px0, p.n_px);
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      const int wv = ((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 0xff;
+      const int bv = ((k < 4 ? bl.x : bl.y) >> (8 * (k & 3))) & 0xff;
+      valid |= uint32_t((wv >= smin) & ((wv - bv) >= cmin) & (px0 + k < p.n_px)) << k;
+    }
+  } else {
+    if (full) {
+      const uint2 mv = *reinterpret_cast<const uint2*>(p.in_mask + px0);
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) valid |= uint32_t((((k < 4 ? mv.x : mv.y) >> (8 * (k & 3))) & 0xff) != 0) << k;
+    } else {
+      for (int k = 0; k < kPx; ++k) valid |= uint32_t(px0 + k < p.n_px && p.in_mask[px0 + k] != 0) << k;
+    }
+  }
+  if (valid) {   // texture early: its latency hides under the code loads
+    const int64_t tb = px0 * 3;
+    if (full) {
+      const uint2* tq = reinterpret_cast<const uint2*>(p.texture + tb);
+      const uint2 t0 = tq[0], t1 = tq[1], t2 = tq[2];
+      tex[0] = t0.x; tex[1] = t0.y; tex[2] = t1.x; tex[3] = t1.y; tex[4] = t2.x; tex[5] = t2.y;
+    } else {
+      for (int k = 0; k < 3 * kPx; ++k)
+        if (tb + k < p.n_px * 3) tex[k >> 2] |= uint32_t(p.texture[tb + k]) << (8 * (k & 3));
+    }
+  }
+  if (SRC_FRAMES) {
+    uint32_t acc[4];
+    decode_axis_mlp(p, p.col_first, p.col_pairs, p.col_pre, p.col_post, px0, full, acc);
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) col[k] = unpack_code(acc, k);
+    if constexpr (ROW_MODE != 0) {
+      decode_axis_mlp(p, p.row_first, p.row_pairs, p.row_pre, p.row_post, px0, full, acc);
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) row[k] = unpack_code(acc, k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) row[k] = 0;
+    }
+  } else {
+    if (full) {
+      const int4* ic = reinterpret_cast<const int4*>(p.in_col + px0);
+      const int4 c0 = ic[0], c1 = ic[1];
+      col[0] = c0.x; col[1] = c0.y; col[2] = c0.z; col[3] = c0.w;
+      col[4] = c1.x; col[5] = c1.y; col[6] = c1.z; col[7] = c1.w;
+      if constexpr (ROW_MODE != 0) {
+        const int4* ir = reinterpret_cast<const int4*>(p.in_row + px0);
+        const int4 r0 = ir[0], r1 = ir[1];
+        row[0] = r0.x; row[1] = r0.y; row[2] = r0.z; row[3] = r0.w;
+        row[4] = r1.x; row[5] = r1.y; row[6] = r1.z; row[7] = r1.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) row[k] = 0;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {
+        const bool in = px0 + k < p.n_px;
+        col[k] = in ? p.in_col[px0 + k] : 0;
+        row[k] = (in && ROW_MODE != 0) ? p.in_row[px0 + k] : 0;
+      }
+    }
+  }
+  // compact the valid pixels of the tile into LDS items (ascending pixel order)
+  const int2 vs = block_scan(__popc(valid), s_tot4);
+  const int n_items = vs.y;
+  {
+    int m = vs.x;
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      if (valid & (1u << k)) {
+        // maps input may hold any int32: clamp like np.clip before packing (processing.py:159)
+        const int c = col[k] < 0 ? 0 : (col[k] > p.n_pcol - 1 ? p.n_pcol - 1 : col[k]);
+        const int r = ROW_MODE == 0 ? 0 : (row[k] < 0 ? 0 : (row[k] > p.n_prow - 1 ? p.n_prow - 1 : row[k]));
+        s_code[m] = uint32_t(c) | (uint32_t(r) << 16);
+        s_off[m] = uint16_t(tid * kPx + k);
+        uint32_t t = 0;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int bi = 3 * k + q;
+          t |= ((tex[bi >> 2] >> (8 * (bi & 3))) & 0xffu) << (8 * q);
+        }
+        s_tex[m] = t;
+        ++m;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------ phase B: triangulate items
+  const int64_t tile_px = int64_t(tile) * kTilePx;
+  const int v0 = int(tile_px / p.width);
+  const int u0 = int(tile_px - int64_t(v0) * p.width);
+  if (p.dbg & 2) {
+    for (int m = tid; m < n_items; m += kBlock) {
+      const uint32_t code = s_code[m];
+      s_xyz[0][3 * m] = XT(code & 0xffff); s_xyz[0][3 * m + 1] = XT(code >> 16); s_xyz[0][3 * m + 2] = XT(m);
+      if constexpr (ROW_MODE == 2) { s_xyz[NS - 1][3 * m] = XT(m); s_xyz[NS - 1][3 * m + 1] = 0; s_xyz[NS - 1][3 * m + 2] = 0; }
+      s_keep[m] = ROW_MODE == 2 ? 3 : 1;
+    }
+  } else {
+    for (int m = tid; m < n_items; m += kBlock) {
+      const uint32_t code = s_code[m];
+      int u = u0 + int(s_off[m]), v = v0;
+      while (u >= p.width) { u -= p.width; ++v; }
+      const double2* qc = reinterpret_cast<const double2*>(p.pcol + 4 * int64_t(code & 0xffffu));
+      const double2 pc01 = qc[0], pc23 = qc[1];
+      double2 pr01 = make_double2(0, 0), pr23 = make_double2(0, 0);
+      if constexpr (ROW_MODE != 0) {
+        const double2* qr = reinterpret_cast<const double2*>(p.prow + 4 * int64_t(code >> 16));
+        pr01 = qr[0]; pr23 = qr[1];
+      }
+      double r0, r1, r2;
+      if (RAYS == SLG_RAYS_PINHOLE) {
+        const double x = (double(u) - p.cx) / p.fx;            // processing.py:150
+        const double y = (double(v) - p.cy) / p.fy;            // processing.py:151
+        const double n = sqrt((x * x + y * y) + 1.0);          // np.linalg.norm(rays, axis=0)
+        r0 = x / n; r1 = y / n; r2 = 1.0 / n;                  // rays /= norms
+      } else {
+        const int64_t px = int64_t(v) * p.width + u;
+        r0 = p.rays[px]; r1 = p.rays[p.n_px + px]; r2 = p.rays[2 * p.n_px + px];
+      }
+      const double den = (pc01.x * r0 + pc01.y * r1) + pc23.x * r2;          // np.sum(N*rays, 0)
+      const double num = ((pc01.x * p.o0 + pc01.y * p.o1) + pc23.x * p.o2) + pc23.y;
+      const bool okc = fabs(den) > 1e-6;
+      const double t = okc ? (-num) / den : 0.0;
+      const double X = p.o0 + r0 * t, Y = p.o1 + r1 * t, Z = p.o2 + r2 * t;
+      uint32_t keep = okc;
+      if constexpr (ROW_MODE == 1) {                          // epipolar filter, processing.py:197-201
+        const double dist = fabs(((pr01.x * X + pr01.y * Y) + pr23.x * Z) + pr23.y);
+        keep = okc && (dist < p.tol);
+      }
+      s_xyz[0][3 * m] = XT(X); s_xyz[0][3 * m + 1] = XT(Y); s_xyz[0][3 * m + 2] = XT(Z);
+      if constexpr (ROW_MODE == 2) {                          // independent row cloud, :218-228
+        const double dr = (pr01.x * r0 + pr01.y * r1) + pr23.x * r2;
+        const double nr = ((pr01.x * p.o0 + pr01.y * p.o1) + pr23.x * p.o2) + pr23.y;
+        const bool okr = fabs(dr) > 1e-6;
+        const double tr = okr ? (-nr) / dr : 0.0;
+        s_xyz[NS - 1][3 * m] = XT(p.o0 + r0 * tr);
+        s_xyz[NS - 1][3 * m + 1] = XT(p.o1 + r1 * tr);
+        s_xyz[NS - 1][3 * m + 2] = XT(p.o2 + r2 * tr);
+        keep |= uint32_t(okr) << 1;
+      }
+      s_keep[m] = uint8_t(keep);
+    }
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------ phase C: ordered output
+#pragma unroll 1
+  for (int stream = 0; stream < NS; ++stream) {
+    const int m0 = tid * kPx;
+    uint32_t kb = 0;
+#pragma unroll
+    for (int k = 0; k < kPx; ++k)
+      if (m0 + k < n_items) kb |= uint32_t((s_keep[m0 + k] >> stream) & 1u) << k;
+    const int2 ks = block_scan(__popc(kb), s_tot4);
+    const int agg = ks.y;
+    {
+      int q = ks.x;
+#pragma unroll
+      for (int k = 0; k < kPx; ++k)
+        if (kb & (1u << k)) s_map[q++] = uint16_t(m0 + k);
+    }
+    uint64_t* st = p.states + int64_t(stream) * p.n_tiles;
+    if (wave == 0) {
+      const uint64_t excl = lookback_prefix(st, tile, agg, p.dbg, &p.ws->error);
+      if ((tid & 63) == 0) {
+        s_excl = excl;
+        if (tile == p.n_tiles - 1) {
+          p.ws->totals[stream] = int64_t(excl) + agg;
+          if (ROW_MODE != 2) *p.count = int64_t(excl) + agg;
+        }
+      }
+    }
+    __syncthreads();
+    if (!(p.dbg & 4)) {
+      const int64_t base = int64_t(s_excl);
+      const XT* sx = s_xyz[stream];
+      XT* gx = reinterpret_cast<XT*>(stream == 0 ? p.xyz : p.scratch_xyz) + base * 3;
+      for (int i = tid; i < agg * 3; i += kBlock) {
+        const int q = i / 3;
+        gx[i] = sx[3 * int(s_map[q]) + (i - 3 * q)];
+      }
+      uint8_t* gb = (stream == 0 ? p.bgr : p.scratch_bgr);
+      const int64_t lo = base * 3, hi = (base + agg) * 3;
+      const int64_t lo4 = (lo + 3) & ~int64_t(3), hi4 = hi & ~int64_t(3);
+      auto byte_at = [&](int64_t b) -> uint32_t {   // b: byte offset inside the tile's BGR run
+        const int q = int(b / 3);
+        return (s_tex[s_map[q]] >> (8 * int(b - 3 * q))) & 0xffu;
+      };
+      if (lo4 < hi4) {
+        for (int64_t i = lo4 + 4 * int64_t(tid); i < hi4; i += 4 * kBlock) {
+          const int64_t b = i - lo;
+          *reinterpret_cast<uint32_t*>(gb + i) =
+              byte_at(b) | (byte_at(b + 1) << 8) | (byte_at(b + 2) << 16) | (byte_at(b + 3) << 24);
+        }
+        if (tid < lo4 - lo) gb[lo + tid] = uint8_t(byte_at(tid));
+        if (tid < hi - hi4) gb[hi4 + tid] = uint8_t(byte_at(hi4 - lo + tid));
+      } else {
+        for (int64_t i = lo + tid; i < hi; i += kBlock) gb[i] = uint8_t(byte_at(i - lo));
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // row_mode 2: append the row cloud (workspace scratch) behind the column cloud.
 template <int XYZ64>
 __global__ __launch_bounds__(kBlock) void row_tail_kernel(WsHeader* ws, const void* sx, const uint8_t* sb,
@@ -851,6 +1193,8 @@ int check_capture(const slg_capture* cap) {
   return SLG_OK;
 }
 
+int debug_flags();
+
 int stats_launch(const uint8_t* white, const uint8_t* black, int64_t n_px, const slg_decode_params* dp,
                  void* workspace, hipStream_t s) {
   StatsParams sp{};
@@ -863,6 +1207,7 @@ int stats_launch(const uint8_t* white, const uint8_t* black, int64_t n_px, const
   sp.thresh_mode = dp ? dp->thresh_mode : SLG_THRESH_MANUAL;
   sp.shadow_val = dp ? dp->shadow_val : 0.0;
   sp.contrast_val = dp ? dp->contrast_val : 0.0;
+  sp.dbg = debug_flags();
   const int64_t chunks = (n_px + kPx - 1) / kPx;
   int64_t grid = (chunks + kBlock - 1) / kBlock;
   if (grid > 512) grid = 512;
@@ -873,8 +1218,16 @@ int stats_launch(const uint8_t* white, const uint8_t* black, int64_t n_px, const
 
 using MainFn = void (*)(MainParams);
 
+int kernel_select() {   // profiling A/B only: SLG_MAIN=1 selects the first-generation kernel
+  const char* e = getenv("SLG_MAIN");
+  return e ? atoi(e) : 2;
+}
+
 template <int RM, int X64, int SRC, int WM, int RAYS>
-MainFn pick5() { return main_kernel<RM, X64, SRC, WM, 1, RAYS>; }
+MainFn pick5() {
+  if (kernel_select() == 1) return main_kernel<RM, X64, SRC, WM, 1, RAYS>;
+  return main2_kernel<RM, X64, SRC, RAYS>;
+}
 
 template <int SRC, int WM>
 MainFn pick_tri(int row_mode, int x64, int rays) {

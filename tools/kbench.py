@@ -86,7 +86,15 @@ def main():
     run("tri_rm1", lambda v: eng.triangulate(maps[v][0], maps[v][1], maps[v][2], dfr[v].texture, dcal, 1,
                                              xyz_f64=False, out=clouds[1]),
         alg_bytes=9 * n_px + 18 * pts[1])
-    for dbg in (1, 2, 4, 3, 7):
+    os.environ["SLG_MAIN"] = "1"
+    run("main_rm1_gen1", lambda v: eng.decode_triangulate(dfr[v], cfg, dcal, clouds[1], 1),
+        pre=lambda v: eng.stats(dfr[v], cfg))
+    run("tri_rm1_gen1", lambda v: eng.triangulate(maps[v][0], maps[v][1], maps[v][2], dfr[v].texture,
+                                                 dcal, 1, xyz_f64=False, out=clouds[1]))
+    os.environ.pop("SLG_MAIN")
+    os.environ["SLG_DBG"] = "16"
+    run("stats_no_otsu", lambda v: eng.stats(dfr[v], cfg))
+    for dbg in (8, 15, 1, 2, 4, 3, 7):
         os.environ["SLG_DBG"] = str(dbg)
         run(f"tri_rm1_dbg{dbg}", lambda v: eng.triangulate(maps[v][0], maps[v][1], maps[v][2], dfr[v].texture,
                                                           dcal, 1, xyz_f64=False, out=clouds[1]))
