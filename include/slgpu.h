@@ -20,6 +20,7 @@
  *                             process_multi_ply._process_source (server/processing.py:286-298)
  *                             without materialising the correspondence maps
  *   slg_decode_triangulate <- the same without the stats launch (after slg_decode_stats)
+ *   slg_ply_write          <- ProcessingLogic._save_ply (server/processing.py:236-248), host side
  *   slg_rays_match_pinhole <- the `Nc.shape[1] == h*w` ray source test
  *                             (server/processing.py:143-156): tells whether the calibration's
  *                             Nc table equals the cam_K pinhole rays bit for bit, in which case
@@ -164,6 +165,13 @@ int32_t slg_decode_triangulate(const slg_capture *cap, const slg_decode_params *
 int32_t slg_rays_match_pinhole(const double *rays, int32_t height, int32_t width, double fx,
                                double fy, double cx, double cy, int64_t *mismatches,
                                void *stream);
+
+/* Host: write an ASCII PLY exactly as ProcessingLogic._save_ply does (processing.py:236-248):
+ * header, then "%.4f %.4f %.4f R G B" per point (Python's correctly rounded formatting, BGR
+ * swapped to RGB).  xyz/bgr are HOST arrays [n][3].  Formats on n_threads host threads
+ * (<= 0: all cores).  Returns bytes written, or -SLG_ERR_* on failure. */
+int64_t slg_ply_write(const char *path, const double *xyz, const uint8_t *bgr, int64_t n,
+                      int32_t n_threads);
 
 #ifdef __cplusplus
 }

@@ -27,6 +27,10 @@
 #include <limits.h>
 #include <type_traits>
 #include <stdlib.h>
+#include <math.h>
+#include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/slgpu.h"
 
@@ -1296,6 +1300,57 @@ int launch_main(MainFn fn, MainParams mp, const slg_tri_params* tp, const slg_cl
   return rc;
 }
 
+// ------------------------------------------------------------------ ASCII PLY (host)
+// "%.4f" of a double exactly as Python formats it (correctly rounded, ties to even, sign of
+// negative zero kept, 'nan' / 'inf' / '-inf'): the value m*2^e times 10^4 is rounded with
+// 128-bit integer arithmetic; magnitudes >= 2^63/10^4 fall back to glibc's exact printf.
+void fmt4(double x, std::string& out) {
+  if (isnan(x)) { out += "nan"; return; }
+  if (isinf(x)) { out += x < 0 ? "-inf" : "inf"; return; }
+  uint64_t bits;
+  memcpy(&bits, &x, 8);
+  const bool neg = bits >> 63;
+  const double ax = fabs(x);
+  if (ax >= 9.2e14) {
+    char buf[400];
+    snprintf(buf, sizeof(buf), "%.4f", x);
+    out += buf;
+    return;
+  }
+  const int bexp = int((bits >> 52) & 0x7ff);
+  uint64_t m = bits & ((uint64_t(1) << 52) - 1);
+  int e;
+  if (bexp == 0) { e = -1074; } else { m |= uint64_t(1) << 52; e = bexp - 1075; }
+  unsigned __int128 v = (unsigned __int128)m * 10000u;
+  uint64_t n;                                   // round(|x| * 10^4), ties to even
+  if (e >= 0) {
+    n = uint64_t(v << e);
+  } else {
+    const int k = -e;
+    if (k >= 127) {
+      n = 0;
+    } else {
+      const unsigned __int128 q = v >> k;
+      const unsigned __int128 rem = v - (q << k);
+      const unsigned __int128 half = (unsigned __int128)1 << (k - 1);
+      n = uint64_t(q) + ((rem > half || (rem == half && (q & 1))) ? 1 : 0);
+    }
+  }
+  char buf[32];
+  int len = snprintf(buf, sizeof(buf), "%s%llu.%04llu", neg ? "-" : "",
+                     (unsigned long long)(n / 10000u), (unsigned long long)(n % 10000u));
+  out.append(buf, size_t(len));
+}
+
+void fmt_u8(unsigned v, std::string& out) {
+  char b[4];
+  int n = 0;
+  if (v >= 100) b[n++] = char('0' + v / 100);
+  if (v >= 10) b[n++] = char('0' + (v / 10) % 10);
+  b[n++] = char('0' + v % 10);
+  out.append(b, size_t(n));
+}
+
 }  // namespace
 
 // ==================================================================== C ABI
@@ -1412,6 +1467,39 @@ int32_t slg_reconstruct(const slg_capture* cap, const slg_decode_params* dp, con
 int32_t slg_decode_triangulate(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,
                                const slg_tri_params* tp, void* workspace, const slg_cloud* out, void* stream) {
   return reconstruct_impl(cap, dp, calib, tp, workspace, out, stream, false);
+}
+
+int64_t slg_ply_write(const char* path, const double* xyz, const uint8_t* bgr, int64_t n, int32_t n_threads) {
+  if (!path || n < 0 || (n > 0 && (!xyz || !bgr))) return -fail(SLG_ERR_INVALID, "bad argument");
+  int nt = n_threads > 0 ? n_threads : int(std::thread::hardware_concurrency());
+  if (nt < 1) nt = 1;
+  if (int64_t(nt) * 4096 > n) nt = int(n / 4096) + 1;
+  std::vector<std::string> parts(static_cast<size_t>(nt));
+  auto work = [&](int t) {
+    const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    std::string& o = parts[size_t(t)];
+    o.reserve(size_t(hi - lo) * 40);
+    for (int64_t i = lo; i < hi; ++i) {
+      fmt4(xyz[3 * i], o); o += ' ';
+      fmt4(xyz[3 * i + 1], o); o += ' ';
+      fmt4(xyz[3 * i + 2], o); o += ' ';
+      fmt_u8(bgr[3 * i + 2], o); o += ' ';        // BGR -> "R G B" (processing.py:248)
+      fmt_u8(bgr[3 * i + 1], o); o += ' ';
+      fmt_u8(bgr[3 * i], o); o += '\n';
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  FILE* f = fopen(path, "wb");
+  if (!f) return -fail(SLG_ERR_INVALID, "cannot open %s", path);
+  int64_t total = fprintf(f, "ply\nformat ascii 1.0\nelement vertex %lld\nproperty float x\nproperty float y\n"
+                             "property float z\nproperty uchar red\nproperty uchar green\nproperty uchar blue\n"
+                             "end_header\n", (long long)n);
+  for (auto& p : parts) total += int64_t(fwrite(p.data(), 1, p.size(), f));
+  if (fclose(f) != 0) return -fail(SLG_ERR_INVALID, "write failed: %s", path);
+  return total;
 }
 
 int32_t slg_rays_match_pinhole(const double* rays, int32_t height, int32_t width, double fx, double fy, double cx,

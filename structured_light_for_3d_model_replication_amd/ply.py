@@ -21,6 +21,15 @@ def format_ascii(points, colors) -> str:
         "%.4f %.4f %.4f %d %d %d\n" % r for r in rows)
 
 
-def write_ascii(filename, points, colors) -> None:
-    with open(filename, "w") as f:
-        f.write(format_ascii(points, colors))
+def write_ascii(filename, points, colors, threads: int = 0) -> None:
+    """Write the PLY with the native multithreaded formatter (``slg_ply_write``)."""
+    import ctypes
+    from . import _native as N
+    P = np.ascontiguousarray(np.asarray(points, dtype=np.float64).reshape(-1, 3))
+    C = np.ascontiguousarray(np.asarray(colors, dtype=np.uint8).reshape(-1, 3))
+    if len(P) != len(C):
+        raise ValueError("points and colors differ in length")
+    rc = N.lib().slg_ply_write(str(filename).encode(), P.ctypes.data_as(ctypes.c_void_p),
+                               C.ctypes.data_as(ctypes.c_void_p), len(P), int(threads))
+    if rc < 0:
+        N.check(-rc)

@@ -102,14 +102,22 @@ def test_ply_bytes_match_reference_writer(tmp_path):
     from structured_light_for_3d_model_replication_amd import ply
     rng = np.random.default_rng(3)
     P = rng.normal(0, 300, (500, 3))
-    P[:5] = [[-0.0, 0.0, 1e-9], [0.00005, 0.00015, -0.00005], [1.23445, 2.5, -2.5],
-             [1e6, -1e6, 123.45675], [0.12345, 0.98765, 5e-5]]
+    P[:9] = [[-0.0, 0.0, 1e-9], [0.00005, 0.00015, -0.00005], [1.23445, 2.5, -2.5],
+             [1e6, -1e6, 123.45675], [0.12345, 0.98765, 5e-5],
+             [0.03125, -0.03125, 2.25e-4],            # exact ties -> round half to even
+             [5e-324, -5e-324, 1e20], [9.3e14, -9.3e14, 1e-300],
+             [np.nan, np.inf, -np.inf]]
     C = rng.integers(0, 256, (500, 3)).astype(np.uint8)
     f = tmp_path / "a.ply"
     ply.write_ascii(str(f), P, C)
     assert f.read_bytes() == O.ply_bytes(P, C)
     ply.write_ascii(str(f), np.zeros((0, 3)), np.zeros((0, 3), np.uint8))
     assert f.read_bytes() == O.ply_bytes(np.zeros((0, 3)), np.zeros((0, 3), np.uint8))
+    big = rng.uniform(-2e3, 2e3, (50000, 3))
+    cb = rng.integers(0, 256, (50000, 3)).astype(np.uint8)
+    for th in (1, 3, 8):                       # chunking across threads keeps the order
+        ply.write_ascii(str(f), big, cb, threads=th)
+        assert f.read_bytes() == O.ply_bytes(big, cb)
 
 
 def test_calibration_tables_match_reference_calibrate_final():
