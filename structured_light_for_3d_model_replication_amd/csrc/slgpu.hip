@@ -380,8 +380,9 @@ struct MainParams {
   int64_t n_tiles;
   void* scratch_xyz;       // row_mode 2 row cloud
   uint8_t* scratch_bgr;
-  int32_t dbg;             // profiling ablations (env SLG_DBG, 0 in production): bit0 no look-back
-                           // wait, bit1 trivial triangulation, bit2 no output stores
+  int32_t dbg;             // env SLG_DBG, 0 in production.  Profiling ablations: bit0 no look-back
+                           // wait, bit1 trivial triangulation, bit2 no output stores; test hook:
+                           // bit5 look-back helps unpublished predecessors immediately
 };
 
 template <int SRC_FRAMES>
@@ -734,63 +735,6 @@ __global__ __launch_bounds__(kBlock) void main_kernel(MainParams p) {
 }
 
 // ------------------------------------------------------------------ main2: LDS-compacted triangulation
-// Exclusive prefix of `agg` over the tiles before `tile` (decoupled look-back; wave 0 calls it,
-// lane 0 publishes).  Waits only for entries newer than the nearest inclusive prefix and
-// re-polls just those, with exponential back-off.
-__device__ uint64_t lookback_prefix(uint64_t* st, int tile, int agg, int dbg, uint32_t* err) {
-  const int lane = threadIdx.x & 63;
-  uint64_t excl = 0;
-  if (dbg & 1) return uint64_t(tile) * kTilePx;               // ablation: no inter-tile wait
-  if (tile == 0) {
-    if (lane == 0) st_state(&st[0], kFlagInc | uint64_t(agg));
-    return 0;
-  }
-  if (lane == 0) st_state(&st[tile], kFlagAgg | uint64_t(agg));
-  int64_t j = tile - 1;
-  for (;;) {
-    uint64_t vv[kLookK];
-#pragma unroll
-    for (int k = 0; k < kLookK; ++k) {
-      const int64_t s = j - (k * 64 + lane);
-      vv[k] = s >= 0 ? ld_state(&st[s]) : kFlagInc;
-    }
-    unsigned spins = 0, nap = 1;
-    int pos;
-    for (;;) {
-      int my_pos = INT_MAX;
-#pragma unroll
-      for (int k = kLookK - 1; k >= 0; --k)
-        if ((vv[k] >> 62) == 2) my_pos = k * 64 + lane;
-      pos = wave_min_i(my_pos);
-      bool ready = true;
-#pragma unroll
-      for (int k = 0; k < kLookK; ++k)
-        if (k * 64 + lane <= pos) ready &= (vv[k] >> 62) != 0;
-      if (__all(ready)) break;
-      if (++spins > kMaxSpin) {
-        if (lane == 0) atomicOr(err, 1u);
-        break;
-      }
-      for (unsigned z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(2);
-      nap = nap < 64 ? nap * 2 : 64;
-#pragma unroll
-      for (int k = 0; k < kLookK; ++k) {
-        const int64_t s = j - (k * 64 + lane);
-        if ((vv[k] >> 62) == 0 && s >= 0 && k * 64 + lane <= pos) vv[k] = ld_state(&st[s]);
-      }
-    }
-    uint64_t sum = 0;
-#pragma unroll
-    for (int k = 0; k < kLookK; ++k)
-      if (k * 64 + lane <= pos) sum += vv[k] & kValMask;
-    excl += wave_sum(sum);
-    if (pos != INT_MAX) break;
-    j -= kLookK * 64;
-  }
-  if (lane == 0) st_state(&st[tile], kFlagInc | (excl + uint64_t(agg)));
-  return excl;
-}
-
 // Block-wide exclusive scan of one int per thread; returns (exclusive, total).
 __device__ inline int2 block_scan(int x, int* s_tot4) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -812,113 +756,69 @@ __device__ inline int2 block_scan(int x, int* s_tot4) {
   return make_int2(off + incl - x, tot);
 }
 
-// Column/row code of all used pairs with every frame load of a batch in flight first.
-__device__ inline void decode_axis_mlp(const MainParams& p, int first, int pairs, int pre, int post,
-                                       int64_t px0, bool full, uint32_t (&acc)[4]) {
-  constexpr int G = 8;
-  acc[0] = acc[1] = acc[2] = acc[3] = 0u;
-  for (int b0 = 0; b0 < pairs; b0 += G) {
-    uint2 pv[G], iv[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      if (b0 + g < pairs) {
-        const uint8_t* fp = p.frames + int64_t(first + 2 * (b0 + g)) * p.stride;
-        if (full) {
-          pv[g] = *reinterpret_cast<const uint2*>(fp + px0);
-          iv[g] = *reinterpret_cast<const uint2*>(fp + p.stride + px0);
-        } else {
-          pv[g] = load8(fp, px0, p.n_px);
-          iv[g] = load8(fp + p.stride, px0, p.n_px);
-        }
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      if (b0 + g < pairs) {
-        const uint32_t m0 = gt_u8x4(pv[g].x, iv[g].x);
-        const uint32_t m1 = gt_u8x4(pv[g].y, iv[g].y);
-        acc[0] = (acc[0] << 1) | ((m0 >> 7) & 0x00010001u);
-        acc[1] = (acc[1] << 1) | ((m0 >> 15) & 0x00010001u);
-        acc[2] = (acc[2] << 1) | ((m1 >> 7) & 0x00010001u);
-        acc[3] = (acc[3] << 1) | ((m1 >> 15) & 0x00010001u);
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = gray2bin_x2(acc[j] << pre) << post;
+__device__ inline void acc_pair(uint32_t (&acc)[4], uint2 pv, uint2 iv) {
+  const uint32_t m0 = gt_u8x4(pv.x, iv.x);
+  const uint32_t m1 = gt_u8x4(pv.y, iv.y);
+  acc[0] = (acc[0] << 1) | ((m0 >> 7) & 0x00010001u);
+  acc[1] = (acc[1] << 1) | ((m0 >> 15) & 0x00010001u);
+  acc[2] = (acc[2] << 1) | ((m1 >> 7) & 0x00010001u);
+  acc[3] = (acc[3] << 1) | ((m1 >> 15) & 0x00010001u);
 }
 
-template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS>
-__global__ __launch_bounds__(kBlock) void main2_kernel(MainParams p) {
-  using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
-  constexpr int NS = ROW_MODE == 2 ? 2 : 1;
-  __shared__ uint32_t s_code[kTilePx];     // valid item m: col | row << 16
-  __shared__ uint16_t s_off[kTilePx];      // pixel offset inside the tile
-  __shared__ uint32_t s_tex[kTilePx];      // B | G << 8 | R << 16
-  __shared__ XT s_xyz[NS][kTilePx * 3];
-  __shared__ uint8_t s_keep[kTilePx];      // bit 0: column stream, bit 1: row stream
-  __shared__ uint16_t s_map[kTilePx];      // output slot -> item
-  __shared__ int s_tot4[4];
-  __shared__ int s_tile;
-  __shared__ uint64_t s_excl;
+__device__ inline uint2 ld_frame8(const MainParams& p, int frame, int64_t px0, bool full) {
+  const uint8_t* fp = p.frames + int64_t(frame) * p.stride;
+  return full ? *reinterpret_cast<const uint2*>(fp + px0) : load8(fp, px0, p.n_px);
+}
 
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  if (tid == 0) s_tile = (p.dbg & 8) ? int(blockIdx.x) : int(atomicAdd(&p.ws->tile_counter, 1u));
-  __syncthreads();
-  const int tile = s_tile;
-  const int64_t px0 = int64_t(tile) * kTilePx + int64_t(tid) * kPx;
-  const bool full = px0 + kPx <= p.n_px;
-
-  // ------------------------------------------------------------ phase A: decode 8 pixels
-  uint32_t valid = 0;
-  int col[kPx], row[kPx];
-  uint32_t tex[6] = {0, 0, 0, 0, 0, 0};
+// Decode the 8 pixels of one lane: mask bits + column / row codes.  Frame loads of both axes
+// are issued up to kBatch pairs at a time before any is consumed (memory-level parallelism).
+template <int ROW_MODE, int SRC_FRAMES, int kBatch>
+__device__ inline void decode_lane(const MainParams& p, int64_t px0, bool full, uint32_t& valid,
+                                   int (&col)[kPx], int (&row)[kPx]) {
+  valid = 0;
   if (SRC_FRAMES) {
     const int smin = p.ws->smin, cmin = p.ws->cmin;
-    const uint2 w = load8(p.frames, px0, p.n_px);
-    const uint2 bl = load8(p.frames + p.stride, px0, p.n_px);
+    const uint2 w = ld_frame8(p, 0, px0, full);
+    const uint2 bl = ld_frame8(p, 1, px0, full);
+    uint32_t ac[4] = {0, 0, 0, 0}, ar[4] = {0, 0, 0, 0};
+    const int np_r = ROW_MODE != 0 ? p.row_pairs : 0;
+    for (int b0 = 0; b0 < max(p.col_pairs, np_r); b0 += kBatch) {
+      uint2 cp[kBatch], ci[kBatch], rp[kBatch], ri[kBatch];
+#pragma unroll
+      for (int g = 0; g < kBatch; ++g)
+        if (b0 + g < p.col_pairs) {
+          cp[g] = ld_frame8(p, p.col_first + 2 * (b0 + g), px0, full);
+          ci[g] = ld_frame8(p, p.col_first + 2 * (b0 + g) + 1, px0, full);
+        }
+#pragma unroll
+      for (int g = 0; g < kBatch; ++g)
+        if (b0 + g < np_r) {
+          rp[g] = ld_frame8(p, p.row_first + 2 * (b0 + g), px0, full);
+          ri[g] = ld_frame8(p, p.row_first + 2 * (b0 + g) + 1, px0, full);
+        }
+#pragma unroll
+      for (int g = 0; g < kBatch; ++g)
+        if (b0 + g < p.col_pairs) acc_pair(ac, cp[g], ci[g]);
+#pragma unroll
+      for (int g = 0; g < kBatch; ++g)
+        if (b0 + g < np_r) acc_pair(ar, rp[g], ri[g]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ac[j] = gray2bin_x2(ac[j] << p.col_pre) << p.col_post;
+      ar[j] = gray2bin_x2(ar[j] << p.row_pre) << p.row_post;
+    }
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
       const int wv = ((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 0xff;
       const int bv = ((k < 4 ? bl.x : bl.y) >> (8 * (k & 3))) & 0xff;
       valid |= uint32_t((wv >= smin) & ((wv - bv) >= cmin) & (px0 + k < p.n_px)) << k;
+      col[k] = unpack_code(ac, k);
+      row[k] = ROW_MODE != 0 ? unpack_code(ar, k) : 0;
     }
   } else {
     if (full) {
       const uint2 mv = *reinterpret_cast<const uint2*>(p.in_mask + px0);
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) valid |= uint32_t((((k < 4 ? mv.x : mv.y) >> (8 * (k & 3))) & 0xff) != 0) << k;
-    } else {
-      for (int k = 0; k < kPx; ++k) valid |= uint32_t(px0 + k < p.n_px && p.in_mask[px0 + k] != 0) << k;
-    }
-  }
-  if (valid) {   // texture early: its latency hides under the code loads
-    const int64_t tb = px0 * 3;
-    if (full) {
-      const uint2* tq = reinterpret_cast<const uint2*>(p.texture + tb);
-      const uint2 t0 = tq[0], t1 = tq[1], t2 = tq[2];
-      tex[0] = t0.x; tex[1] = t0.y; tex[2] = t1.x; tex[3] = t1.y; tex[4] = t2.x; tex[5] = t2.y;
-    } else {
-      for (int k = 0; k < 3 * kPx; ++k)
-        if (tb + k < p.n_px * 3) tex[k >> 2] |= uint32_t(p.texture[tb + k]) << (8 * (k & 3));
-    }
-  }
-  if (SRC_FRAMES) {
-    uint32_t acc[4];
-    decode_axis_mlp(p, p.col_first, p.col_pairs, p.col_pre, p.col_post, px0, full, acc);
-#pragma unroll
-    for (int k = 0; k < kPx; ++k) col[k] = unpack_code(acc, k);
-    if constexpr (ROW_MODE != 0) {
-      decode_axis_mlp(p, p.row_first, p.row_pairs, p.row_pre, p.row_post, px0, full, acc);
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) row[k] = unpack_code(acc, k);
-    } else {
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) row[k] = 0;
-    }
-  } else {
-    if (full) {
       const int4* ic = reinterpret_cast<const int4*>(p.in_col + px0);
       const int4 c0 = ic[0], c1 = ic[1];
       col[0] = c0.x; col[1] = c0.y; col[2] = c0.z; col[3] = c0.w;
@@ -932,97 +832,262 @@ __global__ __launch_bounds__(kBlock) void main2_kernel(MainParams p) {
 #pragma unroll
         for (int k = 0; k < kPx; ++k) row[k] = 0;
       }
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) valid |= uint32_t((((k < 4 ? mv.x : mv.y) >> (8 * (k & 3))) & 0xff) != 0) << k;
     } else {
 #pragma unroll
       for (int k = 0; k < kPx; ++k) {
         const bool in = px0 + k < p.n_px;
         col[k] = in ? p.in_col[px0 + k] : 0;
         row[k] = (in && ROW_MODE != 0) ? p.in_row[px0 + k] : 0;
+        valid |= uint32_t(in && p.in_mask[px0 + k] != 0) << k;
       }
     }
   }
-  // compact the valid pixels of the tile into LDS items (ascending pixel order)
+}
+
+// clamp like np.clip(idx, 0, n-1) (processing.py:159,189) and pack col | row << 16
+template <int ROW_MODE>
+__device__ inline uint32_t pack_code(const MainParams& p, int c, int r) {
+  c = c < 0 ? 0 : (c > p.n_pcol - 1 ? p.n_pcol - 1 : c);
+  r = ROW_MODE == 0 ? 0 : (r < 0 ? 0 : (r > p.n_prow - 1 ? p.n_prow - 1 : r));
+  return uint32_t(c) | (uint32_t(r) << 16);
+}
+
+struct TriOut {
+  double x, y, z;      // column-stream point (row_mode 0/1), or column point (row_mode 2)
+  double rx, ry, rz;   // row-stream point (row_mode 2)
+  uint32_t keep;       // bit 0 column stream, bit 1 row stream
+};
+
+// Ray-plane intersection of one valid pixel (processing.py:143-234), fp64 in NumPy's order.
+template <int ROW_MODE, int RAYS>
+__device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int v) {
+  const double2* qc = reinterpret_cast<const double2*>(p.pcol + 4 * int64_t(code & 0xffffu));
+  const double2 pc01 = qc[0], pc23 = qc[1];
+  double2 pr01 = make_double2(0, 0), pr23 = make_double2(0, 0);
+  if constexpr (ROW_MODE != 0) {
+    const double2* qr = reinterpret_cast<const double2*>(p.prow + 4 * int64_t(code >> 16));
+    pr01 = qr[0];
+    pr23 = qr[1];
+  }
+  double r0, r1, r2;
+  if (RAYS == SLG_RAYS_PINHOLE) {
+    const double x = (double(u) - p.cx) / p.fx;            // processing.py:150
+    const double y = (double(v) - p.cy) / p.fy;            // processing.py:151
+    const double n = sqrt((x * x + y * y) + 1.0);          // np.linalg.norm(rays, axis=0)
+    r0 = x / n; r1 = y / n; r2 = 1.0 / n;                  // rays /= norms
+  } else {
+    const int64_t px = int64_t(v) * p.width + u;
+    r0 = p.rays[px]; r1 = p.rays[p.n_px + px]; r2 = p.rays[2 * p.n_px + px];
+  }
+  TriOut o;
+  const double den = (pc01.x * r0 + pc01.y * r1) + pc23.x * r2;          // np.sum(N*rays, 0)
+  const double num = ((pc01.x * p.o0 + pc01.y * p.o1) + pc23.x * p.o2) + pc23.y;
+  const bool okc = fabs(den) > 1e-6;
+  const double t = okc ? (-num) / den : 0.0;
+  o.x = p.o0 + r0 * t; o.y = p.o1 + r1 * t; o.z = p.o2 + r2 * t;
+  o.keep = okc;
+  o.rx = o.ry = o.rz = 0.0;
+  if constexpr (ROW_MODE == 1) {                          // epipolar filter, processing.py:197-201
+    const double dist = fabs(((pr01.x * o.x + pr01.y * o.y) + pr23.x * o.z) + pr23.y);
+    o.keep = okc && (dist < p.tol);
+  }
+  if constexpr (ROW_MODE == 2) {                          // independent row cloud, :218-228
+    const double dr = (pr01.x * r0 + pr01.y * r1) + pr23.x * r2;
+    const double nr = ((pr01.x * p.o0 + pr01.y * p.o1) + pr23.x * p.o2) + pr23.y;
+    const bool okr = fabs(dr) > 1e-6;
+    const double tr = okr ? (-nr) / dr : 0.0;
+    o.rx = p.o0 + r0 * tr; o.ry = p.o1 + r1 * tr; o.rz = p.o2 + r2 * tr;
+    o.keep |= uint32_t(okr) << 1;
+  }
+  return o;
+}
+
+// Keep-count of another tile, computed by the calling wave alone.  Used only when a
+// predecessor has not published for a long time (it may not have been dispatched yet): the
+// helper publishes the aggregate on its behalf, so the look-back makes progress whatever
+// the dispatch order or other kernels on the device.  Same code path => same value.
+template <int ROW_MODE, int SRC_FRAMES, int RAYS>
+__device__ int tile_keep_count_wave(const MainParams& p, int tile, int stream) {
+  const int lane = threadIdx.x & 63;
+  int cnt = 0;
+  const int64_t tile_px = int64_t(tile) * kTilePx;
+  for (int sub = 0; sub < kBlock / 64; ++sub) {
+    const int64_t px0 = tile_px + int64_t(sub * 64 + lane) * kPx;
+    const bool full = px0 + kPx <= p.n_px;
+    uint32_t valid;
+    int col[kPx], row[kPx];
+    decode_lane<ROW_MODE, SRC_FRAMES, 2>(p, px0, full, valid, col, row);
+    int v = int(px0 / p.width), u = int(px0 - int64_t(v) * p.width);
+    for (int k = 0; k < kPx; ++k) {
+      if (valid & (1u << k)) {
+        const TriOut o = tri_item<ROW_MODE, RAYS>(p, pack_code<ROW_MODE>(p, col[k], row[k]), u, v);
+        cnt += (o.keep >> stream) & 1u;
+      }
+      if (++u == p.width) { u = 0; ++v; }
+    }
+  }
+  return wave_sum(cnt);
+}
+
+constexpr unsigned kHelpAfter = 96;   // back-off rounds (~0.2 ms) before helping a predecessor
+
+// Exclusive prefix of `agg` over the tiles before `tile` (decoupled look-back; wave 0 calls it,
+// lane 0 publishes).  Waits only for entries newer than the nearest inclusive prefix, re-polls
+// just those with exponential back-off, and computes a long-missing predecessor itself.
+template <int ROW_MODE, int SRC_FRAMES, int RAYS>
+__device__ uint64_t lookback_prefix(const MainParams& p, uint64_t* st, int tile, int agg, int stream) {
+  const int lane = threadIdx.x & 63;
+  uint64_t excl = 0;
+  if (p.dbg & 1) return uint64_t(tile) * kTilePx;               // ablation: no inter-tile wait
+  if (tile == 0) {
+    if (lane == 0) st_state(&st[0], kFlagInc | uint64_t(agg));
+    return 0;
+  }
+  if (lane == 0) {   // CAS: a helper may already have published this tile's aggregate
+    unsigned long long expect = 0;
+    __hip_atomic_compare_exchange_strong(reinterpret_cast<unsigned long long*>(&st[tile]), &expect,
+                                         (unsigned long long)(kFlagAgg | uint64_t(agg)), __ATOMIC_RELAXED,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  int64_t j = tile - 1;
+  for (;;) {
+    uint64_t vv[kLookK];
+#pragma unroll
+    for (int k = 0; k < kLookK; ++k) {
+      const int64_t s = j - (k * 64 + lane);
+      vv[k] = s >= 0 ? ld_state(&st[s]) : kFlagInc;
+    }
+    unsigned spins = 0, nap = 1;
+    int pos;
+    for (;;) {
+      int my_pos = INT_MAX;
+#pragma unroll
+      for (int k = kLookK - 1; k >= 0; --k)
+        if ((vv[k] >> 62) == 2) my_pos = k * 64 + lane;
+      pos = wave_min_i(my_pos);
+      int my_miss = INT_MAX;                   // nearest unpublished entry newer than pos
+#pragma unroll
+      for (int k = kLookK - 1; k >= 0; --k)
+        if ((vv[k] >> 62) == 0 && k * 64 + lane <= pos) my_miss = k * 64 + lane;
+      const int miss = wave_min_i(my_miss);
+      if (miss == INT_MAX) break;
+      if (++spins > ((p.dbg & 32) ? 0u : kHelpAfter)) {   // dbg 32: help at once (tests)
+        const int ht = int(j - miss);
+        const int hagg = tile_keep_count_wave<ROW_MODE, SRC_FRAMES, RAYS>(p, ht, stream);
+        if (lane == 0) {
+          unsigned long long expect = 0;
+          __hip_atomic_compare_exchange_strong(reinterpret_cast<unsigned long long*>(&st[ht]), &expect,
+                                               (unsigned long long)(kFlagAgg | uint64_t(hagg)),
+                                               __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          atomicOr(&p.ws->error, 2u);          // diagnostic: a helper ran (not an error)
+        }
+        spins = 0;
+      } else {
+        for (unsigned z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(2);
+        nap = nap < 64 ? nap * 2 : 64;
+      }
+#pragma unroll
+      for (int k = 0; k < kLookK; ++k) {
+        const int64_t s = j - (k * 64 + lane);
+        if ((vv[k] >> 62) == 0 && s >= 0 && k * 64 + lane <= pos) vv[k] = ld_state(&st[s]);
+      }
+    }
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kLookK; ++k)
+      if (k * 64 + lane <= pos) sum += vv[k] & kValMask;
+    excl += wave_sum(sum);
+    if (pos != INT_MAX) break;
+    j -= kLookK * 64;
+  }
+  if (lane == 0) st_state(&st[tile], kFlagInc | (excl + uint64_t(agg)));
+  return excl;
+}
+
+template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS>
+__global__ __launch_bounds__(kBlock) void main2_kernel(MainParams p) {
+  using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
+  constexpr int NS = ROW_MODE == 2 ? 2 : 1;
+  __shared__ uint32_t s_code[kTilePx];     // valid item m: col | row << 16; phase C: keep/map
+  __shared__ uint16_t s_off[kTilePx];      // pixel offset inside the tile
+  __shared__ uint8_t s_tex[kTilePx * 3];   // the tile's BGR bytes (raw pixel order)
+  __shared__ XT s_xyz[NS][kTilePx * 3];
+  __shared__ int s_tot4[4];
+  __shared__ uint64_t s_excl;
+  uint8_t* s_keep = reinterpret_cast<uint8_t*>(s_code);                 // aliases after phase B
+  uint16_t* s_map = reinterpret_cast<uint16_t*>(s_code) + kTilePx;
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int tile = int(blockIdx.x);        // static ids: the look-back helper guarantees progress
+  const int64_t tile_px = int64_t(tile) * kTilePx;
+  const int64_t px0 = tile_px + int64_t(tid) * kPx;
+  const bool full = px0 + kPx <= p.n_px;
+
+  // ------------------------------------------------------------ phase A: decode 8 pixels
+  {
+    const int64_t tb = px0 * 3;            // texture, coalesced, only where it can be needed
+    uint32_t* st32 = reinterpret_cast<uint32_t*>(s_tex);
+    if (full) {
+      const uint2* tq = reinterpret_cast<const uint2*>(p.texture + tb);
+      const uint2 t0 = tq[0], t1 = tq[1], t2 = tq[2];
+      st32[6 * tid + 0] = t0.x; st32[6 * tid + 1] = t0.y; st32[6 * tid + 2] = t1.x;
+      st32[6 * tid + 3] = t1.y; st32[6 * tid + 4] = t2.x; st32[6 * tid + 5] = t2.y;
+    } else {
+      for (int k = 0; k < 3 * kPx; ++k)
+        s_tex[24 * tid + k] = tb + k < p.n_px * 3 ? p.texture[tb + k] : 0;
+    }
+  }
+  uint32_t valid;
+  int col[kPx], row[kPx];
+  decode_lane<ROW_MODE, SRC_FRAMES, 6>(p, px0, full, valid, col, row);
   const int2 vs = block_scan(__popc(valid), s_tot4);
   const int n_items = vs.y;
   {
     int m = vs.x;
 #pragma unroll
-    for (int k = 0; k < kPx; ++k) {
+    for (int k = 0; k < kPx; ++k)
       if (valid & (1u << k)) {
-        // maps input may hold any int32: clamp like np.clip before packing (processing.py:159)
-        const int c = col[k] < 0 ? 0 : (col[k] > p.n_pcol - 1 ? p.n_pcol - 1 : col[k]);
-        const int r = ROW_MODE == 0 ? 0 : (row[k] < 0 ? 0 : (row[k] > p.n_prow - 1 ? p.n_prow - 1 : row[k]));
-        s_code[m] = uint32_t(c) | (uint32_t(r) << 16);
+        s_code[m] = pack_code<ROW_MODE>(p, col[k], row[k]);
         s_off[m] = uint16_t(tid * kPx + k);
-        uint32_t t = 0;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const int bi = 3 * k + q;
-          t |= ((tex[bi >> 2] >> (8 * (bi & 3))) & 0xffu) << (8 * q);
-        }
-        s_tex[m] = t;
         ++m;
       }
-    }
   }
   __syncthreads();
 
   // ------------------------------------------------------------ phase B: triangulate items
-  const int64_t tile_px = int64_t(tile) * kTilePx;
   const int v0 = int(tile_px / p.width);
   const int u0 = int(tile_px - int64_t(v0) * p.width);
-  if (p.dbg & 2) {
-    for (int m = tid; m < n_items; m += kBlock) {
-      const uint32_t code = s_code[m];
-      s_xyz[0][3 * m] = XT(code & 0xffff); s_xyz[0][3 * m + 1] = XT(code >> 16); s_xyz[0][3 * m + 2] = XT(m);
-      if constexpr (ROW_MODE == 2) { s_xyz[NS - 1][3 * m] = XT(m); s_xyz[NS - 1][3 * m + 1] = 0; s_xyz[NS - 1][3 * m + 2] = 0; }
-      s_keep[m] = ROW_MODE == 2 ? 3 : 1;
-    }
-  } else {
-    for (int m = tid; m < n_items; m += kBlock) {
+  uint32_t keepbits = 0;                   // 2 bits per owned item m = tid + 256*i
+#pragma unroll 2
+  for (int i = 0; i < kTilePx / kBlock; ++i) {
+    const int m = tid + kBlock * i;
+    if (m < n_items) {
       const uint32_t code = s_code[m];
       int u = u0 + int(s_off[m]), v = v0;
       while (u >= p.width) { u -= p.width; ++v; }
-      const double2* qc = reinterpret_cast<const double2*>(p.pcol + 4 * int64_t(code & 0xffffu));
-      const double2 pc01 = qc[0], pc23 = qc[1];
-      double2 pr01 = make_double2(0, 0), pr23 = make_double2(0, 0);
-      if constexpr (ROW_MODE != 0) {
-        const double2* qr = reinterpret_cast<const double2*>(p.prow + 4 * int64_t(code >> 16));
-        pr01 = qr[0]; pr23 = qr[1];
-      }
-      double r0, r1, r2;
-      if (RAYS == SLG_RAYS_PINHOLE) {
-        const double x = (double(u) - p.cx) / p.fx;            // processing.py:150
-        const double y = (double(v) - p.cy) / p.fy;            // processing.py:151
-        const double n = sqrt((x * x + y * y) + 1.0);          // np.linalg.norm(rays, axis=0)
-        r0 = x / n; r1 = y / n; r2 = 1.0 / n;                  // rays /= norms
+      uint32_t keep;
+      if (p.dbg & 2) {
+        keep = ROW_MODE == 2 ? 3 : 1;
+        s_xyz[0][3 * m] = XT(code & 0xffff); s_xyz[0][3 * m + 1] = XT(code >> 16); s_xyz[0][3 * m + 2] = XT(u);
+        if constexpr (ROW_MODE == 2) { s_xyz[NS - 1][3 * m] = XT(v); s_xyz[NS - 1][3 * m + 1] = 0; s_xyz[NS - 1][3 * m + 2] = 0; }
       } else {
-        const int64_t px = int64_t(v) * p.width + u;
-        r0 = p.rays[px]; r1 = p.rays[p.n_px + px]; r2 = p.rays[2 * p.n_px + px];
+        const TriOut o = tri_item<ROW_MODE, RAYS>(p, code, u, v);
+        keep = o.keep;
+        s_xyz[0][3 * m] = XT(o.x); s_xyz[0][3 * m + 1] = XT(o.y); s_xyz[0][3 * m + 2] = XT(o.z);
+        if constexpr (ROW_MODE == 2) {
+          s_xyz[NS - 1][3 * m] = XT(o.rx); s_xyz[NS - 1][3 * m + 1] = XT(o.ry); s_xyz[NS - 1][3 * m + 2] = XT(o.rz);
+        }
       }
-      const double den = (pc01.x * r0 + pc01.y * r1) + pc23.x * r2;          // np.sum(N*rays, 0)
-      const double num = ((pc01.x * p.o0 + pc01.y * p.o1) + pc23.x * p.o2) + pc23.y;
-      const bool okc = fabs(den) > 1e-6;
-      const double t = okc ? (-num) / den : 0.0;
-      const double X = p.o0 + r0 * t, Y = p.o1 + r1 * t, Z = p.o2 + r2 * t;
-      uint32_t keep = okc;
-      if constexpr (ROW_MODE == 1) {                          // epipolar filter, processing.py:197-201
-        const double dist = fabs(((pr01.x * X + pr01.y * Y) + pr23.x * Z) + pr23.y);
-        keep = okc && (dist < p.tol);
-      }
-      s_xyz[0][3 * m] = XT(X); s_xyz[0][3 * m + 1] = XT(Y); s_xyz[0][3 * m + 2] = XT(Z);
-      if constexpr (ROW_MODE == 2) {                          // independent row cloud, :218-228
-        const double dr = (pr01.x * r0 + pr01.y * r1) + pr23.x * r2;
-        const double nr = ((pr01.x * p.o0 + pr01.y * p.o1) + pr23.x * p.o2) + pr23.y;
-        const bool okr = fabs(dr) > 1e-6;
-        const double tr = okr ? (-nr) / dr : 0.0;
-        s_xyz[NS - 1][3 * m] = XT(p.o0 + r0 * tr);
-        s_xyz[NS - 1][3 * m + 1] = XT(p.o1 + r1 * tr);
-        s_xyz[NS - 1][3 * m + 2] = XT(p.o2 + r2 * tr);
-        keep |= uint32_t(okr) << 1;
-      }
-      s_keep[m] = uint8_t(keep);
+      keepbits |= keep << (2 * i);
     }
+  }
+  __syncthreads();                                   // s_code no longer needed
+  for (int i = 0; i < kTilePx / kBlock; ++i) {
+    const int m = tid + kBlock * i;
+    if (m < n_items) s_keep[m] = uint8_t((keepbits >> (2 * i)) & 3u);
   }
   __syncthreads();
 
@@ -1044,7 +1109,7 @@ __global__ __launch_bounds__(kBlock) void main2_kernel(MainParams p) {
     }
     uint64_t* st = p.states + int64_t(stream) * p.n_tiles;
     if (wave == 0) {
-      const uint64_t excl = lookback_prefix(st, tile, agg, p.dbg, &p.ws->error);
+      const uint64_t excl = lookback_prefix<ROW_MODE, SRC_FRAMES, RAYS>(p, st, tile, agg, stream);
       if ((tid & 63) == 0) {
         s_excl = excl;
         if (tile == p.n_tiles - 1) {
@@ -1067,7 +1132,7 @@ __global__ __launch_bounds__(kBlock) void main2_kernel(MainParams p) {
       const int64_t lo4 = (lo + 3) & ~int64_t(3), hi4 = hi & ~int64_t(3);
       auto byte_at = [&](int64_t b) -> uint32_t {   // b: byte offset inside the tile's BGR run
         const int q = int(b / 3);
-        return (s_tex[s_map[q]] >> (8 * int(b - 3 * q))) & 0xffu;
+        return s_tex[3 * int(s_off[s_map[q]]) + int(b - 3 * q)];
       };
       if (lo4 < hi4) {
         for (int64_t i = lo4 + 4 * int64_t(tid); i < hi4; i += 4 * kBlock) {

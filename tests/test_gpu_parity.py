@@ -85,7 +85,7 @@ def test_cloud_bit_exact_f64(name, fused, mods):
         assert P.shape == z[f"P{rm}"].shape, (rm, P.shape, z[f"P{rm}"].shape)
         assert np.array_equal(P, z[f"P{rm}"]), f"row_mode {rm}: max |d| {np.abs(P - z[f'P{rm}']).max()}"
         assert np.array_equal(C, z[f"C{rm}"]), f"row_mode {rm} colours"
-        assert eng.error_flags() == 0
+        assert eng.error_flags() & 1 == 0
 
 
 @pytest.mark.parametrize("name", ["proc_otsu_full", "proc_c2style", "proc_odd_geometry", "sl_full"])
@@ -104,6 +104,22 @@ def test_cloud_f32_within_tolerance(name, mods):
         assert len(P) == len(z[f"P{rm}"])
         _xyz32_close(P.cpu().numpy(), z[f"P{rm}"])
         assert np.array_equal(C.cpu().numpy(), z[f"C{rm}"])
+
+
+@pytest.mark.parametrize("name", ["proc_c2style", "proc_odd_geometry", "proc_manual_sets"])
+def test_lookback_helper_path_bit_exact(name, mods, monkeypatch):
+    """Force the look-back to compute unpublished predecessors itself (the progress guarantee
+    used when tiles are dispatched out of order); results must not change."""
+    E, PR, N = mods
+    z = load_case(name)
+    cal = load_calibs()[z["params"]["calib"]]
+    dev = E.DeviceFrames(list(z["frames"]), z["texture"])
+    eng = E.Reconstructor(dev.height, dev.width)
+    dc = E.DeviceCalib(cal, dev.height, dev.width)
+    monkeypatch.setenv("SLG_DBG", "32")
+    for rm in (0, 1, 2):
+        P, C = eng.reconstruct(dev, _cfg(E, z["params"]), dc, row_mode=rm, xyz_f64=True).result()
+        assert np.array_equal(P.cpu().numpy(), z[f"P{rm}"]) and np.array_equal(C.cpu().numpy(), z[f"C{rm}"])
 
 
 def test_ray_table_paths_agree(mods):
@@ -231,7 +247,7 @@ def test_full_size_parity(cam, proj, nsets, thresh, mods):
     P, C = eng.reconstruct(dev, cfg, dc, rm, xyz_f64=True).result()
     Po, Co = O.reconstruct_processing(oc, orow, om, v.texture, cal, row_mode=rm)
     assert np.array_equal(P.cpu().numpy(), Po) and np.array_equal(C.cpu().numpy(), Co)
-    assert eng.error_flags() == 0
+    assert eng.error_flags() & 1 == 0
 
 
 def test_percentile_thresholds_large(mods):
