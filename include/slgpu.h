@@ -20,6 +20,8 @@
  *                             process_multi_ply._process_source (server/processing.py:286-298)
  *                             without materialising the correspondence maps
  *   slg_decode_triangulate <- the same without the stats launch (after slg_decode_stats)
+ *   slg_reconstruct_batch  <- process_multi_ply(mode='batch') over view folders
+ *                             (server/processing.py:314-334): many views, one stream
  *   slg_ply_write          <- ProcessingLogic._save_ply (server/processing.py:236-248), host side
  *   slg_rays_match_pinhole <- the `Nc.shape[1] == h*w` ray source test
  *                             (server/processing.py:143-156): tells whether the calibration's
@@ -36,7 +38,8 @@
  *     message for the last failing call on the calling thread.
  *   - Frames: uint8 [n_frames][frame_stride] planar stack in capture order (index 0 white,
  *     1 black, then (pattern, inverse) per column bit MSB-first, then per row bit starting
- *     at 2 + 2*ceil(log2(proj_cols))).  frame_stride % 8 == 0, base 8-byte aligned.
+ *     at 2 + 2*ceil(log2(proj_cols))).  frame_stride % 8 == 0 and >= round_up(H*W, 8)
+ *     (every frame row is readable in whole 8-byte words), base 8-byte aligned.
  *   - Points are written in ascending pixel order (np.where(mask) order); row_mode 2 writes
  *     the column cloud then the row cloud, like np.hstack((P_col, P_row)).
  */
@@ -73,7 +76,7 @@ extern "C" {
 
 typedef struct slg_capture {
   const uint8_t *frames;   /* device, [n_frames][frame_stride] */
-  int64_t frame_stride;    /* bytes between frames (>= height*width, % 8 == 0) */
+  int64_t frame_stride;    /* bytes between frames (>= round_up(height*width, 8), % 8 == 0) */
   int32_t n_frames;        /* frames present (len(files)) */
   int32_t height;
   int32_t width;
@@ -159,6 +162,16 @@ int32_t slg_reconstruct(const slg_capture *cap, const slg_decode_params *dp,
 int32_t slg_decode_triangulate(const slg_capture *cap, const slg_decode_params *dp,
                                const slg_calib *calib, const slg_tri_params *tp, void *workspace,
                                const slg_cloud *out, void *stream);
+
+/* A batch of views of one geometry (turntable scan, scan farm): one batched stats launch for
+ * all views, then the fused kernels back to back on `stream` (no host sync, no events).
+ * `workspace` holds n_views slices of `ws_stride` bytes (>= slg_workspace_bytes, % 256 == 0),
+ * each initialised once; outs[v] receives view v.  timing_events (optional, 2*n_views
+ * hipEvent_t or NULL entries) are recorded around each fused launch. */
+int32_t slg_reconstruct_batch(const slg_capture *caps, int32_t n_views, const slg_decode_params *dp,
+                              const slg_calib *calib, const slg_tri_params *tp, void *workspace,
+                              int64_t ws_stride, const slg_cloud *outs, void *const *timing_events,
+                              void *stream);
 
 /* Count (into *mismatches, device int64) the Nc entries that differ bitwise from the cam_K
  * pinhole rays; 0 means SLG_RAYS_PINHOLE reproduces the table exactly. */

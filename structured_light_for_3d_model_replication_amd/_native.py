@@ -77,6 +77,9 @@ EXPORTS = {
     "slg_decode_triangulate": (c_i32, [ctypes.POINTER(Capture), ctypes.POINTER(DecodeParams),
                                        ctypes.POINTER(Calib), ctypes.POINTER(TriParams), c_vp,
                                        ctypes.POINTER(Cloud), c_vp]),
+    "slg_reconstruct_batch": (c_i32, [ctypes.POINTER(Capture), c_i32, ctypes.POINTER(DecodeParams),
+                                      ctypes.POINTER(Calib), ctypes.POINTER(TriParams), c_vp, c_i64,
+                                      ctypes.POINTER(Cloud), ctypes.POINTER(c_vp), c_vp]),
     "slg_ply_write": (c_i64, [ctypes.c_char_p, c_vp, c_vp, c_i64, c_i32]),
     "slg_rays_match_pinhole": (c_i32, [c_vp, c_i32, c_i32, c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_vp]),
 }

@@ -62,8 +62,10 @@ struct WsHeader {
   double thr_c;
   int64_t totals[2];       // column / row stream point totals
 };
-constexpr int64_t kHeaderBytes = 8192;
-static_assert(sizeof(WsHeader) <= kHeaderBytes, "header");
+constexpr int kHistCopies = 16;            // partial histograms: blocks spread their atomics
+constexpr int64_t kHistPartOff = 8192;      // uint32 [kHistCopies][2][256] after the header
+constexpr int64_t kHeaderBytes = 65536;
+static_assert(sizeof(WsHeader) <= kHistPartOff, "header");
 
 __host__ __device__ inline int64_t n_tiles_of(int64_t n_px) { return (n_px + kTilePx - 1) / kTilePx; }
 __host__ __device__ inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
@@ -118,13 +120,14 @@ __device__ inline uint2 load8(const uint8_t* base, int64_t px0, int64_t n_px) {
 }
 
 // ------------------------------------------------------------------ stats kernel
+constexpr int kMaxBatch = 16;               // views per batched stats launch (blockIdx.y)
+
 struct StatsParams {
-  const uint8_t* white;
-  const uint8_t* black;
+  const uint8_t* white[kMaxBatch];
+  const uint8_t* black[kMaxBatch];
+  WsHeader* wsv[kMaxBatch];
   int64_t n_px;
-  WsHeader* ws;
-  uint64_t* states;        // zeroed here for the next main launch
-  int64_t n_state_words;
+  int64_t n_state_words;   // look-back words zeroed here for the next main launch
   int32_t thresh_mode;
   int32_t pad;
   double shadow_val;
@@ -244,11 +247,16 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   __shared__ uint32_t s_last;
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
-  WsHeader* ws = p.ws;
+  const int view = blockIdx.y;               // batched launches: one grid row per view
+  WsHeader* ws = p.wsv[view];
+  const uint8_t* white = p.white[view];
+  const uint8_t* black = p.black[view];
+  uint32_t* hist_part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + kHistPartOff);
+  uint64_t* states = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + states_off(p.n_px));
 
   // Arm the compaction state of the following main launch (ordered by the kernel boundary).
   for (int64_t i = int64_t(blockIdx.x) * kBlock + tid; i < p.n_state_words; i += int64_t(gridDim.x) * kBlock)
-    p.states[i] = 0;
+    states[i] = 0;
   if (blockIdx.x == 0 && tid == 0) ws->tile_counter = 0;
 
   if (p.thresh_mode == SLG_THRESH_MANUAL) {
@@ -268,30 +276,45 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   const bool otsu = p.thresh_mode == SLG_THRESH_OTSU;
   uint32_t local_max = 0;
   const int64_t n_chunks = (p.n_px + kPx - 1) / kPx;
-  for (int64_t c = int64_t(blockIdx.x) * kBlock + tid; c < n_chunks; c += int64_t(gridDim.x) * kBlock) {
+  for (int64_t c0 = int64_t(blockIdx.x) * kBlock; c0 < n_chunks; c0 += int64_t(gridDim.x) * kBlock) {
+    const int64_t c = c0 + tid;                 // whole waves iterate together (ballots below)
     const int64_t px0 = c * kPx;
-    const uint2 w = load8(p.white, px0, p.n_px);
-    const uint2 b = load8(p.black, px0, p.n_px);
+    const bool in_chunk = c < n_chunks;
+    const int64_t lp = (in_chunk && px0 < p.n_px) ? px0 : 0;   // rows padded to 8 px
+    const uint2 w = *reinterpret_cast<const uint2*>(white + lp);
+    const uint2 b = *reinterpret_cast<const uint2*>(black + lp);
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
-      if (px0 + k >= p.n_px) break;
+      const bool ok = in_chunk && px0 + k < p.n_px;
       const int wv = ((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 0xff;
       const int bv = ((k < 4 ? b.x : b.y) >> (8 * (k & 3))) & 0xff;
       const int d = wv - bv;
-      if (otsu) {
-        atomicAdd(&sh[wave][0][wv], 1u);
-        atomicAdd(&sh[wave][1][d < 0 ? 0 : d], 1u);
-      } else {
-        atomicAdd(&sh[wave][0][bv], 1u);
-        local_max = max(local_max, uint32_t(d + 256));
+      // Skewed images put many lanes of a wave on one bin (dark background: clip(w-b) = 0);
+      // lanes equal to the first active lane's value are counted with one ballot + one add.
+      const int v0 = otsu ? wv : bv;
+      const int v1 = d < 0 ? 0 : d;
+      const uint64_t act = __ballot(ok);
+      if (act) {
+        const int lead = __ffsll((unsigned long long)act) - 1;
+        const int l0 = __shfl(v0, lead);
+        const uint64_t m0 = __ballot(ok && v0 == l0);
+        if ((threadIdx.x & 63) == lead) atomicAdd(&sh[wave][0][l0], uint32_t(__popcll(m0)));
+        else if (ok && v0 != l0) atomicAdd(&sh[wave][0][v0], 1u);
+        if (otsu) {
+          const int l1 = __shfl(v1, lead);
+          const uint64_t m1 = __ballot(ok && v1 == l1);
+          if ((threadIdx.x & 63) == lead) atomicAdd(&sh[wave][1][l1], uint32_t(__popcll(m1)));
+          else if (ok && v1 != l1) atomicAdd(&sh[wave][1][v1], 1u);
+        }
       }
+      if (!otsu && ok) local_max = max(local_max, uint32_t(d + 256));
     }
   }
   if (!otsu) atomicMax(&s_maxd, local_max);
   __syncthreads();
   for (int i = tid; i < 2 * 256; i += kBlock) {
     const uint32_t v = (&sh[0][0][0])[i] + (&sh[1][0][0])[i] + (&sh[2][0][0])[i] + (&sh[3][0][0])[i];
-    if (v) atomicAdd(&(&ws->hist[0][0])[i], v);
+    if (v) atomicAdd(hist_part + (blockIdx.x % kHistCopies) * 512 + i, v);
   }
   if (!otsu && tid == 0 && s_maxd) atomicMax(&ws->max_diff_enc, s_maxd);
 
@@ -315,7 +338,13 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   __syncthreads();
   uint32_t* hg = &sh[0][0][0];                 // reuse wave-0 slots for the global histograms
   for (int i = tid; i < 2 * 256; i += kBlock)
-    hg[i] = __hip_atomic_load(&(&ws->hist[0][0])[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int c = 0; c < kHistCopies; ++c)
+      acc += __hip_atomic_load(hist_part + c * 512 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hg[i] = acc;
+  }
   if (tid == 0) s_maxd = __hip_atomic_load(&ws->max_diff_enc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (otsu) {
@@ -338,7 +367,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
     const int m = int_threshold(thr, tid == 0 ? 0 : -255);
     if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
   }
-  for (int i = tid; i < 2 * 256; i += kBlock) (&ws->hist[0][0])[i] = 0;
+  for (int i = tid; i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
   if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
 }
 
@@ -765,36 +794,43 @@ __device__ inline void acc_pair(uint32_t (&acc)[4], uint2 pv, uint2 iv) {
   acc[3] = (acc[3] << 1) | ((m1 >> 15) & 0x00010001u);
 }
 
-__device__ inline uint2 ld_frame8(const MainParams& p, int frame, int64_t px0, bool full) {
-  const uint8_t* fp = p.frames + int64_t(frame) * p.stride;
-  return full ? *reinterpret_cast<const uint2*>(fp + px0) : load8(fp, px0, p.n_px);
+// 8 frame bytes at pixel lp (clamped in-bounds by the caller; rows are padded to >= 8 px).
+__device__ inline uint2 ld_frame8(const MainParams& p, int frame, int64_t lp) {
+  return *reinterpret_cast<const uint2*>(p.frames + int64_t(frame) * p.stride + lp);
 }
 
 // Decode the 8 pixels of one lane: mask bits + column / row codes.  Frame loads of both axes
 // are issued up to kBatch pairs at a time before any is consumed (memory-level parallelism).
+// `tail` (wave-uniform) is set only in the last tile, where map/texture reads need guards;
+// frame reads never do: the frame stride is >= round_up(H*W, 8) and out-of-image lanes read
+// pixel 0 (their mask bits are cleared).
 template <int ROW_MODE, int SRC_FRAMES, int kBatch>
-__device__ inline void decode_lane(const MainParams& p, int64_t px0, bool full, uint32_t& valid,
+__device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, uint32_t& valid,
                                    int (&col)[kPx], int (&row)[kPx]) {
   valid = 0;
   if (SRC_FRAMES) {
     const int smin = p.ws->smin, cmin = p.ws->cmin;
-    const uint2 w = ld_frame8(p, 0, px0, full);
-    const uint2 bl = ld_frame8(p, 1, px0, full);
+    const int64_t lp = px0 < p.n_px ? px0 : 0;
+    const uint2 w = ld_frame8(p, 0, lp);
+    const uint2 bl = ld_frame8(p, 1, lp);
     uint32_t ac[4] = {0, 0, 0, 0}, ar[4] = {0, 0, 0, 0};
     const int np_r = ROW_MODE != 0 ? p.row_pairs : 0;
-    for (int b0 = 0; b0 < max(p.col_pairs, np_r); b0 += kBatch) {
+    // compile-time trip count (kMaxBits pairs max), fully unrolled: only forward, wave-uniform
+    // branches remain, so the loads of a batch stay in flight together (no vmcnt(0) per load)
+#pragma unroll
+    for (int b0 = 0; b0 < kMaxBits; b0 += kBatch) {
       uint2 cp[kBatch], ci[kBatch], rp[kBatch], ri[kBatch];
 #pragma unroll
       for (int g = 0; g < kBatch; ++g)
         if (b0 + g < p.col_pairs) {
-          cp[g] = ld_frame8(p, p.col_first + 2 * (b0 + g), px0, full);
-          ci[g] = ld_frame8(p, p.col_first + 2 * (b0 + g) + 1, px0, full);
+          cp[g] = ld_frame8(p, p.col_first + 2 * (b0 + g), lp);
+          ci[g] = ld_frame8(p, p.col_first + 2 * (b0 + g) + 1, lp);
         }
 #pragma unroll
       for (int g = 0; g < kBatch; ++g)
         if (b0 + g < np_r) {
-          rp[g] = ld_frame8(p, p.row_first + 2 * (b0 + g), px0, full);
-          ri[g] = ld_frame8(p, p.row_first + 2 * (b0 + g) + 1, px0, full);
+          rp[g] = ld_frame8(p, p.row_first + 2 * (b0 + g), lp);
+          ri[g] = ld_frame8(p, p.row_first + 2 * (b0 + g) + 1, lp);
         }
 #pragma unroll
       for (int g = 0; g < kBatch; ++g)
@@ -817,7 +853,7 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool full, 
       row[k] = ROW_MODE != 0 ? unpack_code(ar, k) : 0;
     }
   } else {
-    if (full) {
+    if (!tail) {
       const uint2 mv = *reinterpret_cast<const uint2*>(p.in_mask + px0);
       const int4* ic = reinterpret_cast<const int4*>(p.in_col + px0);
       const int4 c0 = ic[0], c1 = ic[1];
@@ -915,10 +951,9 @@ __device__ int tile_keep_count_wave(const MainParams& p, int tile, int stream) {
   const int64_t tile_px = int64_t(tile) * kTilePx;
   for (int sub = 0; sub < kBlock / 64; ++sub) {
     const int64_t px0 = tile_px + int64_t(sub * 64 + lane) * kPx;
-    const bool full = px0 + kPx <= p.n_px;
     uint32_t valid;
     int col[kPx], row[kPx];
-    decode_lane<ROW_MODE, SRC_FRAMES, 2>(p, px0, full, valid, col, row);
+    decode_lane<ROW_MODE, SRC_FRAMES, 4>(p, px0, tile == p.n_tiles - 1, valid, col, row);
     int v = int(px0 / p.width), u = int(px0 - int64_t(v) * p.width);
     for (int k = 0; k < kPx; ++k) {
       if (valid & (1u << k)) {
@@ -1024,13 +1059,13 @@ __global__ __launch_bounds__(kBlock) void main2_kernel(MainParams p) {
   const int tile = int(blockIdx.x);        // static ids: the look-back helper guarantees progress
   const int64_t tile_px = int64_t(tile) * kTilePx;
   const int64_t px0 = tile_px + int64_t(tid) * kPx;
-  const bool full = px0 + kPx <= p.n_px;
+  const bool tail = tile == p.n_tiles - 1;           // wave-uniform: guarded reads only here
 
   // ------------------------------------------------------------ phase A: decode 8 pixels
   {
-    const int64_t tb = px0 * 3;            // texture, coalesced, only where it can be needed
+    const int64_t tb = px0 * 3;            // texture of the tile, coalesced
     uint32_t* st32 = reinterpret_cast<uint32_t*>(s_tex);
-    if (full) {
+    if (!tail) {
       const uint2* tq = reinterpret_cast<const uint2*>(p.texture + tb);
       const uint2 t0 = tq[0], t1 = tq[1], t2 = tq[2];
       st32[6 * tid + 0] = t0.x; st32[6 * tid + 1] = t0.y; st32[6 * tid + 2] = t1.x;
@@ -1042,7 +1077,7 @@ __global__ __launch_bounds__(kBlock) void main2_kernel(MainParams p) {
   }
   uint32_t valid;
   int col[kPx], row[kPx];
-  decode_lane<ROW_MODE, SRC_FRAMES, 6>(p, px0, full, valid, col, row);
+  decode_lane<ROW_MODE, SRC_FRAMES, 8>(p, px0, tail, valid, col, row);
   const int2 vs = block_scan(__popc(valid), s_tot4);
   const int n_items = vs.y;
   {
@@ -1257,21 +1292,25 @@ int check_capture(const slg_capture* cap) {
   if (cap->height < 1 || cap->width < 1) return fail(SLG_ERR_INVALID, "bad image size %dx%d", cap->width, cap->height);
   const int64_t n_px = int64_t(cap->height) * cap->width;
   if (n_px >= (int64_t(1) << 31)) return fail(SLG_ERR_UNSUPPORTED, "image larger than 2^31 pixels");
-  if (cap->frame_stride < n_px || (cap->frame_stride & 7)) return fail(SLG_ERR_INVALID, "frame_stride must be >= H*W and a multiple of 8");
+  if (cap->frame_stride < ((n_px + 7) & ~int64_t(7)) || (cap->frame_stride & 7))
+    return fail(SLG_ERR_INVALID, "frame_stride must be >= round_up(H*W, 8) and a multiple of 8");
   if (reinterpret_cast<uintptr_t>(cap->frames) & 7) return fail(SLG_ERR_INVALID, "frames must be 8-byte aligned");
   return SLG_OK;
 }
 
 int debug_flags();
 
-int stats_launch(const uint8_t* white, const uint8_t* black, int64_t n_px, const slg_decode_params* dp,
-                 void* workspace, hipStream_t s) {
+// One stats launch for n_views views (<= kMaxBatch) of one geometry; view v reads white/black
+// from whites[v] / blacks[v] and owns the workspace slice at workspace + v * ws_stride.
+int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* blacks, int n_views, int64_t n_px,
+                       const slg_decode_params* dp, char* workspace, int64_t ws_stride, hipStream_t s) {
   StatsParams sp{};
-  sp.white = white;
-  sp.black = black;
+  for (int v = 0; v < n_views; ++v) {
+    sp.white[v] = whites ? whites[v] : nullptr;
+    sp.black[v] = blacks ? blacks[v] : nullptr;
+    sp.wsv[v] = reinterpret_cast<WsHeader*>(workspace + int64_t(v) * ws_stride);
+  }
   sp.n_px = n_px;
-  sp.ws = reinterpret_cast<WsHeader*>(workspace);
-  sp.states = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + states_off(n_px));
   sp.n_state_words = 2 * n_tiles_of(n_px);
   sp.thresh_mode = dp ? dp->thresh_mode : SLG_THRESH_MANUAL;
   sp.shadow_val = dp ? dp->shadow_val : 0.0;
@@ -1279,10 +1318,16 @@ int stats_launch(const uint8_t* white, const uint8_t* black, int64_t n_px, const
   sp.dbg = debug_flags();
   const int64_t chunks = (n_px + kPx - 1) / kPx;
   int64_t grid = (chunks + kBlock - 1) / kBlock;
-  if (grid > 512) grid = 512;
+  const int64_t cap = n_views > 1 ? 256 : 512;
+  if (grid > cap) grid = cap;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(stats_kernel, dim3(unsigned(grid)), dim3(kBlock), 0, s, sp);
+  hipLaunchKernelGGL(stats_kernel, dim3(unsigned(grid), unsigned(n_views)), dim3(kBlock), 0, s, sp);
   return check_launch("stats_kernel");
+}
+
+int stats_launch(const uint8_t* white, const uint8_t* black, int64_t n_px, const slg_decode_params* dp,
+                 void* workspace, hipStream_t s) {
+  return stats_launch_batch(&white, &black, 1, n_px, dp, static_cast<char*>(workspace), 0, s);
 }
 
 using MainFn = void (*)(MainParams);
@@ -1565,6 +1610,41 @@ int64_t slg_ply_write(const char* path, const double* xyz, const uint8_t* bgr, i
   for (auto& p : parts) total += int64_t(fwrite(p.data(), 1, p.size(), f));
   if (fclose(f) != 0) return -fail(SLG_ERR_INVALID, "write failed: %s", path);
   return total;
+}
+
+int32_t slg_reconstruct_batch(const slg_capture* caps, int32_t n_views, const slg_decode_params* dp,
+                              const slg_calib* calib, const slg_tri_params* tp, void* workspace,
+                              int64_t ws_stride, const slg_cloud* outs, void* const* timing_events,
+                              void* stream) {
+  if (!caps || n_views < 1 || !dp || !workspace || !outs) return fail(SLG_ERR_INVALID, "NULL argument");
+  const int64_t n_px = int64_t(caps[0].height) * caps[0].width;
+  if (ws_stride < ws_total(n_px) || (ws_stride & 255)) return fail(SLG_ERR_INVALID, "ws_stride too small or not 256-aligned");
+  for (int v = 0; v < n_views; ++v) {
+    int rc = check_capture(&caps[v]);
+    if (rc) return rc;
+    if (caps[v].height != caps[0].height || caps[v].width != caps[0].width)
+      return fail(SLG_ERR_INVALID, "all views of a batch must share one geometry");
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  char* ws = static_cast<char*>(workspace);
+  for (int v0 = 0; v0 < n_views; v0 += kMaxBatch) {
+    const int nb = n_views - v0 < kMaxBatch ? n_views - v0 : kMaxBatch;
+    const uint8_t* wh[kMaxBatch];
+    const uint8_t* bl[kMaxBatch];
+    for (int v = 0; v < nb; ++v) {
+      wh[v] = caps[v0 + v].frames;
+      bl[v] = caps[v0 + v].frames + caps[v0 + v].frame_stride;
+    }
+    int rc = stats_launch_batch(wh, bl, nb, n_px, dp, ws + int64_t(v0) * ws_stride, ws_stride, s);
+    if (rc) return rc;
+    for (int v = v0; v < v0 + nb; ++v) {
+      if (timing_events && timing_events[2 * v]) hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * v]), s);
+      rc = reconstruct_impl(&caps[v], dp, calib, tp, ws + int64_t(v) * ws_stride, &outs[v], stream, false);
+      if (rc) return rc;
+      if (timing_events && timing_events[2 * v + 1]) hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * v + 1]), s);
+    }
+  }
+  return SLG_OK;
 }
 
 int32_t slg_rays_match_pinhole(const double* rays, int32_t height, int32_t width, double fx, double fy, double cx,

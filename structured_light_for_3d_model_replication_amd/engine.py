@@ -284,3 +284,39 @@ class Reconstructor:
     def error_flags(self) -> int:
         hdr = self.workspace[:8192].cpu().numpy()
         return int(np.frombuffer(hdr[3 * 256 * 4 + 12: 3 * 256 * 4 + 16].tobytes(), np.uint32)[0])
+
+
+class BatchReconstructor:
+    """Many views of one geometry per call (``slg_reconstruct_batch``): one batched stats
+    launch, then the fused kernels back to back on one stream.  Owns ``max_views`` workspace
+    slices; ``run`` only enqueues (no host sync)."""
+
+    def __init__(self, height: int, width: int, max_views: int, device=None):
+        self.device = device or default_device()
+        self.height, self.width, self.n_px = int(height), int(width), int(height) * int(width)
+        self.max_views = int(max_views)
+        one = int(N.lib().slg_workspace_bytes(self.n_px))
+        self.ws_stride = (one + 255) // 256 * 256
+        self.workspace = torch.empty(self.ws_stride * self.max_views, dtype=torch.uint8, device=self.device)
+        for v in range(self.max_views):
+            N.check(N.lib().slg_workspace_init(ctypes.c_void_p(self.workspace.data_ptr() + v * self.ws_stride),
+                                               self.ws_stride, _stream()))
+
+    def prepare(self, frames, cfg: DecodeConfig, calib: DeviceCalib, outs, row_mode=1, epipolar_tol=2.0):
+        """Build the argument arrays once (lets a hot loop re-issue the same batch cheaply)."""
+        n = len(frames)
+        if n > self.max_views or len(outs) != n:
+            raise ValueError("batch larger than the engine or outputs/frames mismatch")
+        caps = (N.Capture * n)(*[f.capture() for f in frames])
+        clouds = (N.Cloud * n)(*[o.struct() for o in outs])
+        return (caps, n, cfg.struct(), calib.struct(),
+                N.TriParams(int(row_mode), int(outs[0].xyz_f64), float(epipolar_tol)), clouds)
+
+    def run(self, prepared, events=None, stream=None):
+        caps, n, dp, c, tp, clouds = prepared
+        ev = None
+        if events is not None:
+            ev = (ctypes.c_void_p * (2 * n))(*[int(e) if e else None for e in events])
+        N.check(N.lib().slg_reconstruct_batch(caps, n, ctypes.byref(dp), ctypes.byref(c), ctypes.byref(tp),
+                                              _vp(self.workspace), self.ws_stride, clouds, ev,
+                                              _stream(stream)))

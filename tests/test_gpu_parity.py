@@ -289,3 +289,31 @@ def test_repeated_calls_and_streams(mods):
     for o in outs:
         P, C = o.result()
         assert np.array_equal(P.cpu().numpy(), z["P1"]) and np.array_equal(C.cpu().numpy(), z["C1"])
+
+
+def test_batch_api_matches_single_view(mods):
+    """slg_reconstruct_batch (one batched stats launch + back-to-back fused kernels) gives
+    every view's cloud bit-exactly, including a batch larger than one stats launch (16)."""
+    E, PR, N = mods
+    import torch
+    names = ["proc_otsu_full", "proc_c2style", "proc_missing_odd", "proc_flat_ties", "proc_manual_float"]
+    cal = load_calibs()["rig"]
+    zs = [load_case(n) for n in names]
+    H, W = zs[0]["mask"].shape
+    dc = E.DeviceCalib(cal, H, W)
+    for reps in (1, 4):                                   # 5 and 20 views
+        seq = zs * reps
+        eng = E.BatchReconstructor(H, W, len(seq))
+        frames = [E.DeviceFrames(list(z["frames"]), z["texture"]) for z in seq]
+        # one decode config per batch: run the Otsu ones together, manual separately
+        for cfg_name in ("otsu",):
+            idx = [k for k, z in enumerate(seq) if z["params"].get("thresh_mode", "otsu") == cfg_name
+                   and z["params"].get("n_sets_col", 11) == 11 and z["params"].get("n_sets_row", 11) == 11]
+            fr = [frames[k] for k in idx]
+            outs = [E.Cloud(H * W, 1, True) for _ in idx]
+            eng.run(eng.prepare(fr, E.DecodeConfig(1920, 1080, 11, 11, "otsu"), dc, outs, row_mode=1))
+            torch.cuda.synchronize()
+            for k, o in zip(idx, outs):
+                P, C = o.result()
+                assert np.array_equal(P.cpu().numpy(), seq[k]["P1"]), names[k % len(names)]
+                assert np.array_equal(C.cpu().numpy(), seq[k]["C1"])
