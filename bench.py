@@ -3,15 +3,14 @@
 
 Workload (BASELINE.json configs[1], "C2"): one 1920x1080 view per step, 11 column + 10 row
 Gray-code bits with inverses + white/black (44 frames), Otsu mask, row_mode 1 (epipolar
-filter, tol 2.0), fp32 XYZ + BGR out.  A step = stats launch (histograms -> Otsu thresholds)
-+ the fused decode/triangulate/compaction launch, inputs resident in HBM.  Steps rotate over a
-pool of distinct rendered turntable views (6 x 91 MB frame stacks > 256 MiB Infinity Cache) so
-frames stream from HBM; one view's Otsu overlaps the previous
-view's main kernel: steps are issued in batches of views (slg_reconstruct_batch: one batched
-stats launch for the batch, then the fused kernels back to back on one stream; each step still
-does the full path for its view).  One process per GPU
-(torchrun); each rank renders its own views (weak scaling, no data-path collective);
-value = all ranks' points / max-over-ranks time.
+filter, tol 2.0), fp32 XYZ + BGR out.  Every step does the full path for its view, inputs
+resident in HBM: the stats pass (histograms -> Otsu thresholds) and the fused
+decode/triangulate/compaction pass.  Steps rotate over a pool of distinct rendered turntable
+views (12 x 95 MB frame stacks > 256 MiB Infinity Cache) so frames stream from HBM.  Views are
+issued in batches (C3/C5 style): one fused main3 launch per batch of up to 16 views, with the
+batched stats launch of batch k+1 on a side stream overlapping batch k's fused launch
+(BatchReconstructor.run_pipelined).  One process per GPU (torchrun); each rank renders its own
+views (weak scaling, no data-path collective); value = all ranks' points / max-over-ranks time.
 
 Prints ONE JSON line on stdout (rank 0).  Diagnostics go to stderr.
 """
@@ -70,8 +69,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--views", type=int, default=6)
-    ap.add_argument("--batch", type=int, default=6, help="views per slg_reconstruct_batch call")
+    ap.add_argument("--views", type=int, default=12, help="distinct rendered views in the pool")
+    ap.add_argument("--batch", type=int, default=12, help="views per fused launch (<= 16)")
     ap.add_argument("--xyz", choices=["f32", "f64"], default="f32")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -103,68 +102,70 @@ def main():
     row_mode, tol, f64 = 1, 2.0, args.xyz == "f64"
     dframes = [E.DeviceFrames(list(v.frames), v.texture, device=dev) for v in views]
     dcal = E.DeviceCalib(cal, H, W, device=dev)
-    B = max(1, min(args.batch, len(views)))
+    B = max(1, min(args.batch, E.MAX_VIEWS_PER_LAUNCH))
     s_main = torch.cuda.Stream(device=dev)
-    beng = E.BatchReconstructor(H, W, B, device=dev)
-    clouds = [E.Cloud(H * W, row_mode, f64, device=dev) for _ in range(B)]
-    # batches cycle through the view pool; prepared argument arrays per (batch start, size)
+    s_stats = torch.cuda.Stream(device=dev)
+    beng = E.BatchReconstructor(H, W, B, device=dev, slots=2)
+    clouds = [[E.Cloud(H * W, row_mode, f64, device=dev) for _ in range(B)] for _ in range(2)]
     preps = {}
 
-    def prep(start, n):
-        key = (start, n)
+    def prep(start, n, slot):
+        """Batch of n consecutive pool views from `start` on workspace/cloud slot `slot`."""
+        key = (start, n, slot)
         if key not in preps:
             fr = [dframes[(start + k) % len(views)] for k in range(n)]
-            preps[key] = beng.prepare(fr, cfg, dcal, clouds[:n], row_mode, tol)
+            preps[key] = beng.prepare(fr, cfg, dcal, clouds[slot][:n], row_mode, tol, slot=slot)
         return preps[key]
 
-    # points per view (also a sanity check of the GPU result against the pool)
+    # points per view (and a sanity pass over the pool)
     pts = []
     for v in range(len(views)):
-        beng.run(prep(v, 1), stream=s_main)
+        beng.run(prep(v, 1, 0), stream=s_main)
         s_main.synchronize()
-        pts.append(int(clouds[0].count.item()))
+        pts.append(int(clouds[0][0].count.item()))
 
-    K, Wm = args.steps, args.warmup
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)]
-    for e in ev:                                   # materialise the HIP events
-        e.record(s_main)
-    torch.cuda.synchronize()
-    total_pts = 0
-    bytes_alg = 0.0
-    out_b = 30 if f64 else 18            # 3 B texture read + 12|24 B XYZ + 3 B BGR per point
-    frame_b = (2 + 2 * (11 + 10)) * H * W
-
-    def run_steps(first, count, timed):
-        """Steps [first, first+count) in batches of B views; returns views processed."""
-        done = []
-        j = 0
+    def batches_for(first, count):
+        """Steps [first, first+count) as batches of <= B views on alternating slots."""
+        out, j = [], 0
         while j < count:
             n = min(B, count - j)
-            start = (first + j) % len(views)
-            evs = [ev[2 * (first - Wm + j + k) + h].cuda_event for k in range(n) for h in (0, 1)] if timed else None
-            beng.run(prep(start, n), events=evs, stream=s_main)
-            done += [(start + k) % len(views) for k in range(n)]
+            out.append(prep((first + j) % len(views), n, len(out) % 2))
             j += n
-        return done
+        return out
 
-    run_steps(0, Wm, False)
+    K, Wm = args.steps, args.warmup
+    warm = batches_for(0, Wm)
+    timed = batches_for(Wm, K)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in timed]
+    for a, b in ev:                                  # materialise the HIP events
+        a.record(s_main)
+        b.record(s_main)
+    torch.cuda.synchronize()
+    out_b = 30 if f64 else 18            # 3 B texture read + 12|24 B XYZ + 3 B BGR per point
+    frame_b = (2 + 2 * (11 + 10)) * H * W
+    total_pts, bytes_alg = 0, 0.0
+    for v in range(Wm, Wm + K):
+        total_pts += pts[v % len(views)]
+        bytes_alg += frame_b + out_b * pts[v % len(views)]
+
+    if warm:
+        beng.run_pipelined(warm, s_main, s_stats)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for v in run_steps(Wm, K, True):
-        total_pts += pts[v]
-        bytes_alg += frame_b + out_b * pts[v]
+    beng.run_pipelined(timed, s_main, s_stats, events=[(a.cuda_event, b.cuda_event) for a, b in ev])
     t_enq = time.perf_counter() - t0              # host time to enqueue the K steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    kern_ms = sum(ev[2 * j].elapsed_time(ev[2 * j + 1]) for j in range(K))
-    hdr = [beng.workspace[k * beng.ws_stride: k * beng.ws_stride + 8192].cpu().numpy() for k in range(B)]
-    helper_runs = sum(int(np.frombuffer(h[3084:3088].tobytes(), np.uint32)[0] & 2 != 0) for h in hdr)
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev)
+    n_launch = len(ev)
+    helper_runs = sum(int(np.frombuffer(beng.header(s, k)[3084:3088].cpu().numpy().tobytes(), np.uint32)[0] & 2 != 0)
+                      for s in range(2) for k in range(B))
 
     stats = torch.tensor([dt, float(total_pts), kern_ms, bytes_alg], dtype=torch.float64, device=dev)
     if world > 1:
@@ -178,12 +179,13 @@ def main():
         dt_max, all_pts, kern_sum, bytes_sum = dt, float(total_pts), kern_ms, bytes_alg
 
     if rank == 0:
-        launches = K * world
+        launches = n_launch * world
         kern_avg_s = kern_sum / launches / 1e3
         achieved = bytes_sum / launches / kern_avg_s / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(),
-                "kernel": "main_kernel<1,0,1,0,1,1> (fused decode+triangulate+compaction)",
+                "kernel": "main3_kernel<1,0,1,1> (fused decode+triangulate+compaction, "
+                          f"{B} views per launch)",
                 "kernel_avg_us": round(kern_avg_s * 1e6, 2),
                 "alg_bytes_per_launch": round(bytes_sum / launches)}
         cpu = None
@@ -207,6 +209,7 @@ def main():
                                    f"{args.xyz} + BGR out",
                        "views_per_rank": len(views), "points_per_view": int(np.mean(pts)),
                        "batch_views": B,
+                       "launches": n_launch,
                        "lookback_helper_runs": helper_runs,
                        "host_enqueue_ms_per_step": round(t_enq / K * 1e3, 4),
                        "decode": "u8 compares, int32 codes; triangulation f64",

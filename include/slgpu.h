@@ -163,15 +163,26 @@ int32_t slg_decode_triangulate(const slg_capture *cap, const slg_decode_params *
                                const slg_calib *calib, const slg_tri_params *tp, void *workspace,
                                const slg_cloud *out, void *stream);
 
-/* A batch of views of one geometry (turntable scan, scan farm): one batched stats launch for
- * all views, then the fused kernels back to back on `stream` (no host sync, no events).
- * `workspace` holds n_views slices of `ws_stride` bytes (>= slg_workspace_bytes, % 256 == 0),
- * each initialised once; outs[v] receives view v.  timing_events (optional, 2*n_views
- * hipEvent_t or NULL entries) are recorded around each fused launch. */
+/* A batch of views of one geometry (turntable scan, scan farm; frame counts may differ):
+ * per group of up to 16 views, one batched stats launch and ONE fused decode+triangulate launch
+ * covering every view of the group (no host sync).  `workspace` holds n_views slices of
+ * `ws_stride` bytes (>= slg_workspace_bytes, % 256 == 0), each initialised once; outs[v]
+ * receives view v.  timing_events (optional: NULL, or 2 hipEvent_t / NULL entries per group of
+ * 16 views) are recorded around each fused launch. */
 int32_t slg_reconstruct_batch(const slg_capture *caps, int32_t n_views, const slg_decode_params *dp,
                               const slg_calib *calib, const slg_tri_params *tp, void *workspace,
                               int64_t ws_stride, const slg_cloud *outs, void *const *timing_events,
                               void *stream);
+
+/* The two halves of slg_reconstruct_batch, so a caller can run the stats of the next batch on a
+ * second stream while this batch's fused launch runs (each view's workspace slice must not be
+ * shared between the two batches in flight). */
+int32_t slg_decode_stats_batch(const slg_capture *caps, int32_t n_views, const slg_decode_params *dp,
+                               void *workspace, int64_t ws_stride, void *stream);
+int32_t slg_decode_triangulate_batch(const slg_capture *caps, int32_t n_views, const slg_decode_params *dp,
+                                     const slg_calib *calib, const slg_tri_params *tp, void *workspace,
+                                     int64_t ws_stride, const slg_cloud *outs, void *const *timing_events,
+                                     void *stream);
 
 /* Count (into *mismatches, device int64) the Nc entries that differ bitwise from the cam_K
  * pinhole rays; 0 means SLG_RAYS_PINHOLE reproduces the table exactly. */

@@ -14,6 +14,8 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_NAME = "libslgpu.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+if os.environ.get("SLG_LIB"):            # A/B builds of the same ABI (tools/kbench.py); in-tree only
+    LIB_PATH = os.path.abspath(os.environ["SLG_LIB"])
 
 SLG_OK = 0
 SLG_ERR_INVALID = 1
@@ -80,6 +82,11 @@ EXPORTS = {
     "slg_reconstruct_batch": (c_i32, [ctypes.POINTER(Capture), c_i32, ctypes.POINTER(DecodeParams),
                                       ctypes.POINTER(Calib), ctypes.POINTER(TriParams), c_vp, c_i64,
                                       ctypes.POINTER(Cloud), ctypes.POINTER(c_vp), c_vp]),
+    "slg_decode_stats_batch": (c_i32, [ctypes.POINTER(Capture), c_i32, ctypes.POINTER(DecodeParams),
+                                       c_vp, c_i64, c_vp]),
+    "slg_decode_triangulate_batch": (c_i32, [ctypes.POINTER(Capture), c_i32, ctypes.POINTER(DecodeParams),
+                                             ctypes.POINTER(Calib), ctypes.POINTER(TriParams), c_vp,
+                                             c_i64, ctypes.POINTER(Cloud), ctypes.POINTER(c_vp), c_vp]),
     "slg_ply_write": (c_i64, [ctypes.c_char_p, c_vp, c_vp, c_i64, c_i32]),
     "slg_rays_match_pinhole": (c_i32, [c_vp, c_i32, c_i32, c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_vp]),
 }

@@ -8,11 +8,13 @@
 //   stats_kernel      white/black histograms (+ max contrast) -> last-arriving workgroup turns
 //                     them into integer mask thresholds (Otsu as OpenCV, or NumPy percentile);
 //                     also zeroes the compaction state of the next main launch.
-//   main_kernel<...>  one 2048-pixel tile per workgroup (256 lanes x 8 pixels): streams the
+//   main3_kernel<...> fused decode + triangulate + ordered compaction, one 2048-pixel tile per
+//                     workgroup (256 lanes x 8 pixels), up to 16 views per launch: streams the
 //                     used frames with 8-byte-per-lane coalesced loads, SWAR byte compares,
-//                     packed 16-bit Gray->binary, optional map stores, fp64 ray-plane
-//                     intersection, ordered compaction (block scan + decoupled look-back over
-//                     dynamic tile ids) staged through LDS and written with coalesced stores.
+//                     packed 16-bit Gray->binary, wave-private LDS compaction of valid pixels,
+//                     fp64 ray-plane intersection, decoupled look-back over in-order claimed
+//                     tiles, compacted stores straight from registers.
+//   decode_maps_kernel  the decode alone, to correspondence maps (slg_decode).
 //   row_tail_kernel   row_mode 2: moves the row cloud behind the column cloud.
 //   pinhole_kernel    bitwise Nc == pinhole(cam_K) test.
 //
@@ -42,18 +44,17 @@ constexpr int kBlock = 256;                 // 4 waves of 64
 constexpr int kPx = 8;                      // pixels per lane (one 8-byte load per frame)
 constexpr int kTilePx = kBlock * kPx;       // 2048 pixels per workgroup tile
 constexpr int kMaxBits = 15;                // packed 16-bit code lanes
-constexpr int kLookK = 16;                  // look-back window = 16 x 64 predecessor tiles
+constexpr int kLookK = 2;                  // look-back window = 2 x 64 predecessor tiles per poll
 constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagInc = 2ull << 62;
 constexpr uint64_t kValMask = (1ull << 62) - 1;
-constexpr unsigned kMaxSpin = 1u << 22;
 
 // ------------------------------------------------------------------ workspace layout
 struct WsHeader {
   uint32_t hist[3][256];   // otsu: 0 white, 1 clip(white-black,0,255); percentile: 0 black
   uint32_t max_diff_enc;   // max(white-black) + 256 (0 = none yet)
   uint32_t ticket;         // stats_kernel arrival counter
-  uint32_t tile_counter;   // dynamic tile id for main_kernel
+  uint32_t tile_counter;   // next (view, tile) id of a main3 launch (this slice = its view 0)
   uint32_t error;          // bit 0: look-back spin timeout
   int32_t smin;            // mask: white >= smin
   int32_t cmin;            //       (white - black) >= cmin
@@ -70,7 +71,8 @@ static_assert(sizeof(WsHeader) <= kHistPartOff, "header");
 __host__ __device__ inline int64_t n_tiles_of(int64_t n_px) { return (n_px + kTilePx - 1) / kTilePx; }
 __host__ __device__ inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 __host__ __device__ inline int64_t states_off(int64_t) { return kHeaderBytes; }
-__host__ __device__ inline int64_t states_bytes(int64_t n_px) { return align_up(2 * n_tiles_of(n_px) * 8, 256); }
+__host__ __device__ inline int64_t n_state_words(int64_t n_px) { return 2 * n_tiles_of(n_px); }   // [stream][tile]
+__host__ __device__ inline int64_t states_bytes(int64_t n_px) { return align_up(n_state_words(n_px) * 8, 256); }
 __host__ __device__ inline int64_t scratch_xyz_off(int64_t n_px) { return kHeaderBytes + states_bytes(n_px); }
 __host__ __device__ inline int64_t scratch_bgr_off(int64_t n_px) { return scratch_xyz_off(n_px) + align_up(n_px * 24, 256); }
 __host__ __device__ inline int64_t ws_total(int64_t n_px) { return scratch_bgr_off(n_px) + align_up(n_px * 3, 256); }
@@ -110,17 +112,9 @@ __device__ inline uint32_t gray2bin_x2(uint32_t x) {
   return x;
 }
 
-// 8 bytes of a plane starting at pixel px0; tail-safe.
-__device__ inline uint2 load8(const uint8_t* base, int64_t px0, int64_t n_px) {
-  if (px0 + kPx <= n_px) return *reinterpret_cast<const uint2*>(base + px0);
-  uint32_t w[2] = {0u, 0u};
-  for (int k = 0; k < kPx; ++k)
-    if (px0 + k < n_px) w[k >> 2] |= uint32_t(base[px0 + k]) << (8 * (k & 3));
-  return make_uint2(w[0], w[1]);
-}
-
 // ------------------------------------------------------------------ stats kernel
 constexpr int kMaxBatch = 16;               // views per batched stats launch (blockIdx.y)
+constexpr int kStatsPx = 32;                // pixels per lane per stats iteration
 
 struct StatsParams {
   const uint8_t* white[kMaxBatch];
@@ -272,22 +266,27 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   if (tid == 0) s_maxd = 0;
   __syncthreads();
 
-  // hist slots: otsu -> [0] white, [1] clip(white-black); percentile -> [0] black
+  // hist slots: otsu -> [0] white, [1] clip(white-black); percentile -> [0] black.
+  // Each lane takes kStatsPx consecutive pixels (all loads issued before any is consumed).
   const bool otsu = p.thresh_mode == SLG_THRESH_OTSU;
   uint32_t local_max = 0;
-  const int64_t n_chunks = (p.n_px + kPx - 1) / kPx;
-  for (int64_t c0 = int64_t(blockIdx.x) * kBlock; c0 < n_chunks; c0 += int64_t(gridDim.x) * kBlock) {
-    const int64_t c = c0 + tid;                 // whole waves iterate together (ballots below)
-    const int64_t px0 = c * kPx;
-    const bool in_chunk = c < n_chunks;
-    const int64_t lp = (in_chunk && px0 < p.n_px) ? px0 : 0;   // rows padded to 8 px
-    const uint2 w = *reinterpret_cast<const uint2*>(white + lp);
-    const uint2 b = *reinterpret_cast<const uint2*>(black + lp);
+  const int64_t per_block = int64_t(kBlock) * kStatsPx;
+  for (int64_t b0 = int64_t(blockIdx.x) * per_block; b0 < p.n_px; b0 += int64_t(gridDim.x) * per_block) {
+    const int64_t px0 = b0 + int64_t(tid) * kStatsPx;  // whole waves iterate together (ballots below)
+    const int64_t lp = px0 < p.n_px ? px0 : 0;           // frames are readable up to round_up(n, 8)
+    uint2 w[kStatsPx / 8], b[kStatsPx / 8];
 #pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      const bool ok = in_chunk && px0 + k < p.n_px;
-      const int wv = ((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 0xff;
-      const int bv = ((k < 4 ? b.x : b.y) >> (8 * (k & 3))) & 0xff;
+    for (int q = 0; q < kStatsPx / 8; ++q) {
+      const int64_t o = lp + 8 * q < p.n_px ? lp + 8 * q : 0;
+      w[q] = *reinterpret_cast<const uint2*>(white + o);
+      b[q] = *reinterpret_cast<const uint2*>(black + o);
+    }
+#pragma unroll
+    for (int k = 0; k < kStatsPx; ++k) {
+      const bool ok = px0 + k < p.n_px;
+      const uint2 wq = w[k >> 3], bq = b[k >> 3];
+      const int wv = (((k & 7) < 4 ? wq.x : wq.y) >> (8 * (k & 3))) & 0xff;
+      const int bv = (((k & 7) < 4 ? bq.x : bq.y) >> (8 * (k & 3))) & 0xff;
       const int d = wv - bv;
       // Skewed images put many lanes of a wave on one bin (dark background: clip(w-b) = 0);
       // lanes equal to the first active lane's value are counted with one ballot + one add.
@@ -414,377 +413,13 @@ struct MainParams {
                            // bit5 look-back helps unpublished predecessors immediately
 };
 
-template <int SRC_FRAMES>
-__device__ inline void decode_axis(const MainParams& p, int first, int pairs, int pre, int post,
-                                   int64_t px0, uint32_t (&acc)[4]) {
-  acc[0] = acc[1] = acc[2] = acc[3] = 0u;
-  for (int b = 0; b < pairs; ++b) {
-    const uint8_t* fp = p.frames + int64_t(first + 2 * b) * p.stride;
-    const uint2 pv = load8(fp, px0, p.n_px);
-    const uint2 iv = load8(fp + p.stride, px0, p.n_px);
-    const uint32_t m0 = gt_u8x4(pv.x, iv.x);
-    const uint32_t m1 = gt_u8x4(pv.y, iv.y);
-    acc[0] = (acc[0] << 1) | ((m0 >> 7) & 0x00010001u);
-    acc[1] = (acc[1] << 1) | ((m0 >> 15) & 0x00010001u);
-    acc[2] = (acc[2] << 1) | ((m1 >> 7) & 0x00010001u);
-    acc[3] = (acc[3] << 1) | ((m1 >> 15) & 0x00010001u);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = gray2bin_x2(acc[j] << pre) << post;
-}
-
 // code of pixel k (0..7) from the packed accumulators
 __device__ inline int unpack_code(const uint32_t (&acc)[4], int k) {
   const uint32_t a = acc[((k >> 2) << 1) | (k & 1)];
   return int((a >> (16 * ((k >> 1) & 1))) & 0xffffu);
 }
 
-struct Pt {
-  double x, y, z;
-};
-
-__device__ inline double ray_plane_denom(const double4& pl, double r0, double r1, double r2) {
-  return (pl.x * r0 + pl.y * r1) + pl.z * r2;                 // np.sum(N * rays, axis=0)
-}
-
-__device__ inline double4 load_plane(const double* tab, int n, int idx) {
-  idx = idx < 0 ? 0 : (idx > n - 1 ? n - 1 : idx);            // np.clip(idx, 0, n-1)
-  const double2* q = reinterpret_cast<const double2*>(tab + 4 * int64_t(idx));
-  const double2 a = q[0], b = q[1];
-  return make_double4(a.x, a.y, b.x, b.y);
-}
-
-template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int WRITE_MAPS, int TRI, int RAYS>
-__global__ __launch_bounds__(kBlock) void main_kernel(MainParams p) {
-  using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
-  constexpr int kStageXyz = TRI ? kTilePx * 3 : 1;
-  __shared__ XT s_xyz[kStageXyz];
-  __shared__ uint8_t s_bgr[TRI ? kTilePx * 3 : 4];
-  __shared__ int s_wave_tot[4];
-  __shared__ int s_tile;
-  __shared__ uint64_t s_excl;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-
-  int tile;
-  if (TRI) {
-    if (tid == 0) s_tile = int(atomicAdd(&p.ws->tile_counter, 1u));
-    __syncthreads();
-    tile = s_tile;
-  } else {
-    tile = blockIdx.x;
-  }
-  const int64_t px0 = int64_t(tile) * kTilePx + int64_t(tid) * kPx;
-
-  // -------------------------------------------------------------- decode 8 pixels
-  uint32_t valid = 0;   // bit k: mask of pixel k
-  int col[kPx], row[kPx];
-  if (SRC_FRAMES) {
-    const int smin = p.ws->smin, cmin = p.ws->cmin;
-    const uint2 w = load8(p.frames, px0, p.n_px);
-    const uint2 bl = load8(p.frames + p.stride, px0, p.n_px);
-#pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      const int wv = ((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 0xff;
-      const int bv = ((k < 4 ? bl.x : bl.y) >> (8 * (k & 3))) & 0xff;
-      const bool ok = (wv >= smin) & ((wv - bv) >= cmin) & (px0 + k < p.n_px);
-      valid |= uint32_t(ok) << k;
-    }
-    uint32_t acc[4];
-    decode_axis<1>(p, p.col_first, p.col_pairs, p.col_pre, p.col_post, px0, acc);
-#pragma unroll
-    for (int k = 0; k < kPx; ++k) col[k] = unpack_code(acc, k);
-    if (ROW_MODE != 0 || WRITE_MAPS) {
-      decode_axis<1>(p, p.row_first, p.row_pairs, p.row_pre, p.row_post, px0, acc);
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) row[k] = unpack_code(acc, k);
-    } else {
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) row[k] = 0;
-    }
-    if (WRITE_MAPS) {
-      if (px0 + kPx <= p.n_px) {
-        int4* oc = reinterpret_cast<int4*>(p.out_col + px0);
-        int4* orr = reinterpret_cast<int4*>(p.out_row + px0);
-        oc[0] = make_int4(col[0], col[1], col[2], col[3]);
-        oc[1] = make_int4(col[4], col[5], col[6], col[7]);
-        orr[0] = make_int4(row[0], row[1], row[2], row[3]);
-        orr[1] = make_int4(row[4], row[5], row[6], row[7]);
-        uint32_t m0 = 0, m1 = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          m0 |= ((valid >> k) & 1u) << (8 * k);
-          m1 |= ((valid >> (k + 4)) & 1u) << (8 * k);
-        }
-        *reinterpret_cast<uint2*>(p.out_mask + px0) = make_uint2(m0, m1);
-      } else {
-        for (int k = 0; k < kPx; ++k)
-          if (px0 + k < p.n_px) {
-            p.out_col[px0 + k] = col[k];
-            p.out_row[px0 + k] = row[k];
-            p.out_mask[px0 + k] = uint8_t((valid >> k) & 1u);
-          }
-      }
-    }
-  } else {
-    if (px0 + kPx <= p.n_px) {
-      const int4* ic = reinterpret_cast<const int4*>(p.in_col + px0);
-      const int4 c0 = ic[0], c1 = ic[1];
-      col[0] = c0.x; col[1] = c0.y; col[2] = c0.z; col[3] = c0.w;
-      col[4] = c1.x; col[5] = c1.y; col[6] = c1.z; col[7] = c1.w;
-      if (ROW_MODE != 0) {
-        const int4* ir = reinterpret_cast<const int4*>(p.in_row + px0);
-        const int4 r0 = ir[0], r1 = ir[1];
-        row[0] = r0.x; row[1] = r0.y; row[2] = r0.z; row[3] = r0.w;
-        row[4] = r1.x; row[5] = r1.y; row[6] = r1.z; row[7] = r1.w;
-      } else {
-#pragma unroll
-        for (int k = 0; k < kPx; ++k) row[k] = 0;
-      }
-      const uint2 mv = *reinterpret_cast<const uint2*>(p.in_mask + px0);
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) valid |= uint32_t((((k < 4 ? mv.x : mv.y) >> (8 * (k & 3))) & 0xff) != 0) << k;
-    } else {
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) {
-        const bool in = px0 + k < p.n_px;
-        col[k] = in ? p.in_col[px0 + k] : 0;
-        row[k] = (in && ROW_MODE != 0) ? p.in_row[px0 + k] : 0;
-        valid |= uint32_t(in && p.in_mask[px0 + k] != 0) << k;
-      }
-    }
-  }
-  if (!TRI) return;
-
-  // -------------------------------------------------------------- triangulate
-  uint32_t keep_c = 0, keep_r = 0;
-  XT xc[kPx][3], xr[ROW_MODE == 2 ? kPx : 1][3];
-  uint32_t tex[6] = {0, 0, 0, 0, 0, 0};   // 24 bytes BGR of the 8 pixels
-  if (valid) {
-    const int64_t tb = px0 * 3;
-    if (px0 + kPx <= p.n_px) {
-      const uint2* tq = reinterpret_cast<const uint2*>(p.texture + tb);
-      const uint2 t0 = tq[0], t1 = tq[1], t2 = tq[2];
-      tex[0] = t0.x; tex[1] = t0.y; tex[2] = t1.x; tex[3] = t1.y; tex[4] = t2.x; tex[5] = t2.y;
-    } else {
-      for (int k = 0; k < 3 * kPx; ++k)
-        if (px0 * 3 + k < p.n_px * 3) tex[k >> 2] |= uint32_t(p.texture[tb + k]) << (8 * (k & 3));
-    }
-    int v = int(px0 / p.width);
-    int u = int(px0 - int64_t(v) * p.width);
-    if (p.dbg & 2) {
-      keep_c = valid;
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) { xc[k][0] = XT(col[k]); xc[k][1] = XT(row[k]); xc[k][2] = XT(u + k); }
-      if constexpr (ROW_MODE == 2) {
-        keep_r = valid;
-#pragma unroll
-        for (int k = 0; k < kPx; ++k) { xr[k][0] = XT(row[k]); xr[k][1] = XT(col[k]); xr[k][2] = XT(v); }
-      }
-    } else
-#pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      if (valid & (1u << k)) {
-        double r0, r1, r2;
-        if (RAYS == SLG_RAYS_PINHOLE) {
-          const double x = (double(u) - p.cx) / p.fx;           // processing.py:150
-          const double y = (double(v) - p.cy) / p.fy;           // processing.py:151
-          const double n = sqrt((x * x + y * y) + 1.0);         // np.linalg.norm(axis=0)
-          r0 = x / n; r1 = y / n; r2 = 1.0 / n;                 // rays /= norms
-        } else {
-          const int64_t px = px0 + k;
-          r0 = p.rays[px];
-          r1 = p.rays[p.n_px + px];
-          r2 = p.rays[2 * p.n_px + px];
-        }
-        const double4 pc = load_plane(p.pcol, p.n_pcol, col[k]);
-        const double den = ray_plane_denom(pc, r0, r1, r2);
-        const double num = ((pc.x * p.o0 + pc.y * p.o1) + pc.z * p.o2) + pc.w;
-        const bool okc = fabs(den) > 1e-6;
-        const double t = okc ? (-num) / den : 0.0;
-        const double X = p.o0 + r0 * t, Y = p.o1 + r1 * t, Z = p.o2 + r2 * t;
-        bool kc = okc;
-        if constexpr (ROW_MODE == 1) {
-          const double4 pr = load_plane(p.prow, p.n_prow, row[k]);
-          const double dist = fabs(((pr.x * X + pr.y * Y) + pr.z * Z) + pr.w);
-          kc = okc && (dist < p.tol);
-        }
-        if (kc) {
-          keep_c |= 1u << k;
-          xc[k][0] = XT(X); xc[k][1] = XT(Y); xc[k][2] = XT(Z);
-        }
-        if constexpr (ROW_MODE == 2) {
-          const double4 pr = load_plane(p.prow, p.n_prow, row[k]);
-          const double dr = ray_plane_denom(pr, r0, r1, r2);
-          const double nr = ((pr.x * p.o0 + pr.y * p.o1) + pr.z * p.o2) + pr.w;
-          if (fabs(dr) > 1e-6) {
-            const double tr = (-nr) / dr;
-            keep_r |= 1u << k;
-            xr[k][0] = XT(p.o0 + r0 * tr); xr[k][1] = XT(p.o1 + r1 * tr); xr[k][2] = XT(p.o2 + r2 * tr);
-          }
-        }
-      }
-      if (++u == p.width) { u = 0; ++v; }
-    }
-  }
-
-  // -------------------------------------------------------------- ordered compaction
-#pragma unroll 1
-  for (int stream = 0; stream < (ROW_MODE == 2 ? 2 : 1); ++stream) {
-    const uint32_t keep = stream == 0 ? keep_c : keep_r;
-    const int cnt = __popc(keep);
-    // inclusive wave scan
-    int incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
-    }
-    if (lane == 63) s_wave_tot[wave] = incl;
-    __syncthreads();
-    int wave_off = 0, agg = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      wave_off += (w < wave) ? s_wave_tot[w] : 0;
-      agg += s_wave_tot[w];
-    }
-    const int local = wave_off + incl - cnt;
-
-    // stage the lane's points into LDS at their compacted slot
-    {
-      int j = local;
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) {
-        if (keep & (1u << k)) {
-          if constexpr (ROW_MODE == 2) {
-            const XT* src = stream == 0 ? xc[k] : xr[k];
-            s_xyz[3 * j + 0] = src[0]; s_xyz[3 * j + 1] = src[1]; s_xyz[3 * j + 2] = src[2];
-          } else {
-            s_xyz[3 * j + 0] = xc[k][0]; s_xyz[3 * j + 1] = xc[k][1]; s_xyz[3 * j + 2] = xc[k][2];
-          }
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const int bi = 3 * k + c;
-            s_bgr[3 * j + c] = uint8_t((tex[bi >> 2] >> (8 * (bi & 3))) & 0xff);
-          }
-          ++j;
-        }
-      }
-    }
-
-    // tile prefix: decoupled look-back by wave 0
-    uint64_t* st = p.states + int64_t(stream) * p.n_tiles;
-    if (wave == 0) {
-      uint64_t excl = 0;
-      if (p.dbg & 1) {
-        excl = uint64_t(tile) * kTilePx;                     // ablation: no inter-tile wait
-      } else if (tile == 0) {
-        if (lane == 0) st_state(&st[0], kFlagInc | uint64_t(agg));
-      } else {
-        if (lane == 0) st_state(&st[tile], kFlagAgg | uint64_t(agg));
-        int64_t j = tile - 1;
-        for (;;) {
-          uint64_t vv[kLookK];
-#pragma unroll
-          for (int k = 0; k < kLookK; ++k) {
-            const int64_t s = j - (k * 64 + lane);
-            vv[k] = s >= 0 ? ld_state(&st[s]) : kFlagInc;
-          }
-          // Wait only for entries newer than the nearest inclusive prefix; re-poll just the
-          // missing ones, with exponential back-off so waiting tiles do not flood the fabric.
-          unsigned spins = 0, nap = 1;
-          int pos;
-          for (;;) {
-            int my_pos = INT_MAX;
-#pragma unroll
-            for (int k = kLookK - 1; k >= 0; --k)
-              if ((vv[k] >> 62) == 2) my_pos = k * 64 + lane;
-            pos = wave_min_i(my_pos);
-            bool ready = true;
-#pragma unroll
-            for (int k = 0; k < kLookK; ++k)
-              if (k * 64 + lane <= pos) ready &= (vv[k] >> 62) != 0;
-            if (__all(ready)) break;
-            if (++spins > kMaxSpin) {
-              if (lane == 0) atomicOr(&p.ws->error, 1u);
-              break;
-            }
-            for (unsigned z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(2);
-            nap = nap < 64 ? nap * 2 : 64;
-#pragma unroll
-            for (int k = 0; k < kLookK; ++k) {
-              const int64_t s = j - (k * 64 + lane);
-              if ((vv[k] >> 62) == 0 && s >= 0 && k * 64 + lane <= pos) vv[k] = ld_state(&st[s]);
-            }
-          }
-          uint64_t sum = 0;
-#pragma unroll
-          for (int k = 0; k < kLookK; ++k)
-            if (k * 64 + lane <= pos) sum += vv[k] & kValMask;
-          excl += wave_sum(sum);
-          if (pos != INT_MAX) break;
-          j -= kLookK * 64;
-        }
-        if (lane == 0) st_state(&st[tile], kFlagInc | (excl + uint64_t(agg)));
-      }
-      if (lane == 0) {
-        s_excl = excl;
-        if (tile == p.n_tiles - 1) {
-          p.ws->totals[stream] = int64_t(excl) + agg;
-          if (ROW_MODE != 2) *p.count = int64_t(excl) + agg;
-        }
-      }
-    }
-    __syncthreads();
-    const int64_t base = int64_t(s_excl);
-
-    if (p.dbg & 4) { __syncthreads(); continue; }
-    // coalesced copy-out of the tile's compacted points
-    XT* gx = reinterpret_cast<XT*>(stream == 0 ? p.xyz : p.scratch_xyz) + base * 3;
-    for (int i = tid; i < agg * 3; i += kBlock) gx[i] = s_xyz[i];
-    uint8_t* gb = (stream == 0 ? p.bgr : p.scratch_bgr);
-    const int64_t lo = base * 3, hi = (base + agg) * 3;
-    const int64_t lo4 = (lo + 3) & ~int64_t(3), hi4 = hi & ~int64_t(3);
-    if (lo4 < hi4) {
-      for (int64_t i = lo4 + 4 * int64_t(tid); i < hi4; i += 4 * kBlock) {
-        const int64_t s = i - lo;
-        const uint32_t v = uint32_t(s_bgr[s]) | (uint32_t(s_bgr[s + 1]) << 8) |
-                           (uint32_t(s_bgr[s + 2]) << 16) | (uint32_t(s_bgr[s + 3]) << 24);
-        *reinterpret_cast<uint32_t*>(gb + i) = v;
-      }
-      if (tid < lo4 - lo) gb[lo + tid] = s_bgr[tid];
-      if (tid < hi - hi4) gb[hi4 + tid] = s_bgr[hi4 - lo + tid];
-    } else {
-      for (int64_t i = lo + tid; i < hi; i += kBlock) gb[i] = s_bgr[i - lo];
-    }
-    __syncthreads();   // LDS reuse by the next stream
-  }
-}
-
-// ------------------------------------------------------------------ main2: LDS-compacted triangulation
-// Block-wide exclusive scan of one int per thread; returns (exclusive, total).
-__device__ inline int2 block_scan(int x, int* s_tot4) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int incl = x;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o);
-    if (lane >= o) incl += y;
-  }
-  if (lane == 63) s_tot4[wave] = incl;
-  __syncthreads();
-  int off = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    off += (w < wave) ? s_tot4[w] : 0;
-    tot += s_tot4[w];
-  }
-  __syncthreads();
-  return make_int2(off + incl - x, tot);
-}
-
+// ------------------------------------------------------------------ decode (shared by the kernels)
 __device__ inline void acc_pair(uint32_t (&acc)[4], uint2 pv, uint2 iv) {
   const uint32_t m0 = gt_u8x4(pv.x, iv.x);
   const uint32_t m1 = gt_u8x4(pv.y, iv.y);
@@ -940,52 +575,80 @@ __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int
   return o;
 }
 
-// Keep-count of another tile, computed by the calling wave alone.  Used only when a
-// predecessor has not published for a long time (it may not have been dispatched yet): the
-// helper publishes the aggregate on its behalf, so the look-back makes progress whatever
-// the dispatch order or other kernels on the device.  Same code path => same value.
+// One pixel decoded exactly as decode_lane decodes it, with byte loads and few registers
+// (the look-back helper path only).
+template <int ROW_MODE, int SRC_FRAMES>
+__device__ inline bool decode_px(const MainParams& p, int64_t px, int& col, int& row) {
+  if (SRC_FRAMES) {
+    const uint8_t* f = p.frames + px;
+    const int wv = f[0], bv = f[p.stride];
+    uint32_t c = 0, r = 0;
+    for (int b = 0; b < p.col_pairs; ++b)
+      c = (c << 1) | uint32_t(f[int64_t(p.col_first + 2 * b) * p.stride] > f[int64_t(p.col_first + 2 * b + 1) * p.stride]);
+    col = int(gray2bin_x2(c << p.col_pre) << p.col_post);
+    if (ROW_MODE != 0) {
+      for (int b = 0; b < p.row_pairs; ++b)
+        r = (r << 1) | uint32_t(f[int64_t(p.row_first + 2 * b) * p.stride] > f[int64_t(p.row_first + 2 * b + 1) * p.stride]);
+      r = gray2bin_x2(r << p.row_pre) << p.row_post;
+    }
+    row = int(r);
+    return (wv >= p.ws->smin) & ((wv - bv) >= p.ws->cmin);
+  }
+  col = p.in_col[px];
+  row = ROW_MODE != 0 ? p.in_row[px] : 0;
+  return p.in_mask[px] != 0;
+}
+
+// Keep-count of another tile of the same view, computed by the calling wave alone: the
+// aggregate a predecessor that has not published for a long time would publish (it may not
+// have been dispatched yet).  Same arithmetic as main3's phases A/B => same value.
 template <int ROW_MODE, int SRC_FRAMES, int RAYS>
 __device__ int tile_keep_count_wave(const MainParams& p, int tile, int stream) {
   const int lane = threadIdx.x & 63;
   int cnt = 0;
   const int64_t tile_px = int64_t(tile) * kTilePx;
-  for (int sub = 0; sub < kBlock / 64; ++sub) {
-    const int64_t px0 = tile_px + int64_t(sub * 64 + lane) * kPx;
-    uint32_t valid;
-    int col[kPx], row[kPx];
-    decode_lane<ROW_MODE, SRC_FRAMES, 4>(p, px0, tile == p.n_tiles - 1, valid, col, row);
-    int v = int(px0 / p.width), u = int(px0 - int64_t(v) * p.width);
-    for (int k = 0; k < kPx; ++k) {
-      if (valid & (1u << k)) {
-        const TriOut o = tri_item<ROW_MODE, RAYS>(p, pack_code<ROW_MODE>(p, col[k], row[k]), u, v);
-        cnt += (o.keep >> stream) & 1u;
-      }
-      if (++u == p.width) { u = 0; ++v; }
+#pragma unroll 1
+  for (int i = lane; i < kTilePx; i += 64) {
+    const int64_t px = tile_px + i;
+    int col, row;
+    if (px < p.n_px && decode_px<ROW_MODE, SRC_FRAMES>(p, px, col, row)) {
+      const int v = int(px / p.width), u = int(px - int64_t(v) * p.width);
+      const TriOut o = tri_item<ROW_MODE, RAYS>(p, pack_code<ROW_MODE>(p, col, row), u, v);
+      cnt += (o.keep >> stream) & 1u;
     }
   }
   return wave_sum(cnt);
 }
 
-constexpr unsigned kHelpAfter = 96;   // back-off rounds (~0.2 ms) before helping a predecessor
+__device__ inline void publish_agg(uint64_t* w, int agg) {   // unless a helper already did
+  unsigned long long expect = 0;
+  __hip_atomic_compare_exchange_strong(reinterpret_cast<unsigned long long*>(w), &expect,
+                                       (unsigned long long)(kFlagAgg | uint64_t(agg)), __ATOMIC_RELAXED,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-// Exclusive prefix of `agg` over the tiles before `tile` (decoupled look-back; wave 0 calls it,
-// lane 0 publishes).  Waits only for entries newer than the nearest inclusive prefix, re-polls
-// just those with exponential back-off, and computes a long-missing predecessor itself.
-template <int ROW_MODE, int SRC_FRAMES, int RAYS>
-__device__ uint64_t lookback_prefix(const MainParams& p, uint64_t* st, int tile, int agg, int stream) {
+constexpr unsigned kNapCap = 8;         // back-off cap: 8 x s_sleep(2) ~ 1k clocks between re-polls
+constexpr unsigned kHelpAfter = 2048;   // s_sleep(2) units (~0.1 ms) before asking for help
+
+// Decoupled look-back over static tile ids (wave 0 calls it, lane 0 publishes).  Returns true
+// with the exclusive prefix of `agg` over the view's tiles before `tile`, or false with the
+// nearest predecessor that has not published for kHelpAfter (it may not be dispatched yet:
+// dispatch order is not guaranteed): the caller then computes that tile's aggregate itself
+// (tile_keep_count_wave) and retries, so waiting always ends.  Re-polls only the entries
+// newer than the nearest inclusive prefix, with capped back-off.
+__device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int agg, uint64_t& excl_out,
+                             int& help_tile) {
   const int lane = threadIdx.x & 63;
-  uint64_t excl = 0;
-  if (p.dbg & 1) return uint64_t(tile) * kTilePx;               // ablation: no inter-tile wait
+  if (p.dbg & 1) { excl_out = uint64_t(tile) * kTilePx; return true; }   // ablation: no wait
   if (tile == 0) {
     if (lane == 0) st_state(&st[0], kFlagInc | uint64_t(agg));
-    return 0;
+    excl_out = 0;
+    return true;
   }
-  if (lane == 0) {   // CAS: a helper may already have published this tile's aggregate
-    unsigned long long expect = 0;
-    __hip_atomic_compare_exchange_strong(reinterpret_cast<unsigned long long*>(&st[tile]), &expect,
-                                         (unsigned long long)(kFlagAgg | uint64_t(agg)), __ATOMIC_RELAXED,
-                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (lane == 0) st_state(&st[tile], kFlagAgg | uint64_t(agg));   // a helper only ever writes this same value
+  const unsigned nap_cap = (p.dbg >> 8) & 0xff ? (p.dbg >> 8) & 0xff : kNapCap;   // dbg bits 8-15: A/B
+  const unsigned help_after = (p.dbg & 32) ? 0u : kHelpAfter;                       // dbg 32: tests
+  uint64_t excl = 0;
   int64_t j = tile - 1;
   for (;;) {
     uint64_t vv[kLookK];
@@ -994,7 +657,7 @@ __device__ uint64_t lookback_prefix(const MainParams& p, uint64_t* st, int tile,
       const int64_t s = j - (k * 64 + lane);
       vv[k] = s >= 0 ? ld_state(&st[s]) : kFlagInc;
     }
-    unsigned spins = 0, nap = 1;
+    unsigned slept = 0, nap = 1;
     int pos;
     for (;;) {
       int my_pos = INT_MAX;
@@ -1008,21 +671,13 @@ __device__ uint64_t lookback_prefix(const MainParams& p, uint64_t* st, int tile,
         if ((vv[k] >> 62) == 0 && k * 64 + lane <= pos) my_miss = k * 64 + lane;
       const int miss = wave_min_i(my_miss);
       if (miss == INT_MAX) break;
-      if (++spins > ((p.dbg & 32) ? 0u : kHelpAfter)) {   // dbg 32: help at once (tests)
-        const int ht = int(j - miss);
-        const int hagg = tile_keep_count_wave<ROW_MODE, SRC_FRAMES, RAYS>(p, ht, stream);
-        if (lane == 0) {
-          unsigned long long expect = 0;
-          __hip_atomic_compare_exchange_strong(reinterpret_cast<unsigned long long*>(&st[ht]), &expect,
-                                               (unsigned long long)(kFlagAgg | uint64_t(hagg)),
-                                               __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          atomicOr(&p.ws->error, 2u);          // diagnostic: a helper ran (not an error)
-        }
-        spins = 0;
-      } else {
-        for (unsigned z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(2);
-        nap = nap < 64 ? nap * 2 : 64;
+      if (slept >= help_after) {
+        help_tile = int(j - miss);
+        return false;
       }
+      for (unsigned z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(2);
+      slept += nap;
+      nap = nap < nap_cap ? nap * 2 : nap_cap;
 #pragma unroll
       for (int k = 0; k < kLookK; ++k) {
         const int64_t s = j - (k * 64 + lane);
@@ -1038,150 +693,267 @@ __device__ uint64_t lookback_prefix(const MainParams& p, uint64_t* st, int tile,
     j -= kLookK * 64;
   }
   if (lane == 0) st_state(&st[tile], kFlagInc | (excl + uint64_t(agg)));
-  return excl;
+  excl_out = excl;
+  return true;
+}
+
+// Correspondence maps of one 2048-pixel tile (slg_decode): col/row int32, mask uint8.
+__global__ __launch_bounds__(kBlock) void decode_maps_kernel(MainParams p) {
+  const int64_t px0 = int64_t(blockIdx.x) * kTilePx + int64_t(threadIdx.x) * kPx;
+  const bool tail = int64_t(blockIdx.x) == p.n_tiles - 1;
+  uint32_t valid;
+  int col[kPx], row[kPx];
+  decode_lane<1, 1, 8>(p, px0, tail, valid, col, row);
+  if (px0 + kPx <= p.n_px) {
+    int4* oc = reinterpret_cast<int4*>(p.out_col + px0);
+    int4* orr = reinterpret_cast<int4*>(p.out_row + px0);
+    oc[0] = make_int4(col[0], col[1], col[2], col[3]);
+    oc[1] = make_int4(col[4], col[5], col[6], col[7]);
+    orr[0] = make_int4(row[0], row[1], row[2], row[3]);
+    orr[1] = make_int4(row[4], row[5], row[6], row[7]);
+    uint32_t m0 = 0, m1 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      m0 |= ((valid >> k) & 1u) << (8 * k);
+      m1 |= ((valid >> (k + 4)) & 1u) << (8 * k);
+    }
+    *reinterpret_cast<uint2*>(p.out_mask + px0) = make_uint2(m0, m1);
+  } else {
+    for (int k = 0; k < kPx; ++k)
+      if (px0 + k < p.n_px) {
+        p.out_col[px0 + k] = col[k];
+        p.out_row[px0 + k] = row[k];
+        p.out_mask[px0 + k] = uint8_t((valid >> k) & 1u);
+      }
+  }
+}
+
+// ------------------------------------------------------------------ main3: occupancy-first fused kernel
+// One launch covers up to kMaxViews views of one geometry (grid = views x tiles, view-major).
+// Per 256-lane workgroup and 2048-pixel tile:
+//  A  every lane decodes its 8 pixels (all used frames in flight, 8-byte coalesced loads); a
+//     block scan compacts the tile's valid pixels into LDS items (code, BGR, pixel offset);
+//  B  the 256 lanes triangulate the items 256 at a time (fp64, NumPy order) -- balanced over
+//     the four waves whatever the foreground layout; points stay in registers and one ballot
+//     per wave and round gives every kept point its rank;
+//  C  one barrier shares the per-(round, wave) counts, wave 0 resolves the tile's offset by
+//     decoupled look-back (helping a long-silent predecessor, so waiting always ends);
+//  D  each lane stores its points at offset + rank: consecutive lanes write consecutive
+//     points, so the compacted stores coalesce without an LDS staging copy.
+// 20 KB of LDS and no point staging keep several workgroups per CU resident, so one tile's
+// decode stream overlaps other tiles' fp64 work and look-back.
+constexpr int kMaxViews = 16;
+#ifndef SLG_M3_WAVES
+#define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
+#endif
+
+struct ViewIO {
+  const uint8_t* frames;      // SRC_FRAMES: [F][stride]
+  const uint8_t* texture;     // [n_px][3] BGR
+  const int32_t* in_col;      // !SRC_FRAMES: maps
+  const int32_t* in_row;
+  const uint8_t* in_mask;
+  void* xyz;
+  uint8_t* bgr;
+  int64_t* count;
+  WsHeader* ws;
+  uint64_t* states;           // [2][n_tiles]
+  void* scratch_xyz;          // row_mode 2 row cloud
+  uint8_t* scratch_bgr;
+  int64_t stride;             // frame stride of this view
+  int32_t col_first, col_pairs, col_pre, col_post;   // decode plan of this view (frames present)
+  int32_t row_first, row_pairs, row_pre, row_post;
+};
+
+struct Main3Params {
+  MainParams c;               // geometry, decode plan, calibration (per-view pointers unused)
+  int32_t n_views;
+  int32_t pad;
+  ViewIO v[kMaxViews];
+};
+
+__device__ inline MainParams view_params(const Main3Params& P, int view) {
+  MainParams q = P.c;
+  const ViewIO& io = P.v[view];
+  q.frames = io.frames; q.texture = io.texture;
+  q.in_col = io.in_col; q.in_row = io.in_row; q.in_mask = io.in_mask;
+  q.xyz = io.xyz; q.bgr = io.bgr; q.count = io.count;
+  q.ws = io.ws; q.states = io.states;
+  q.scratch_xyz = io.scratch_xyz; q.scratch_bgr = io.scratch_bgr;
+  q.stride = io.stride;
+  q.col_first = io.col_first; q.col_pairs = io.col_pairs; q.col_pre = io.col_pre; q.col_post = io.col_post;
+  q.row_first = io.row_first; q.row_pairs = io.row_pairs; q.row_pre = io.row_pre; q.row_post = io.row_post;
+  return q;
+}
+
+// BGR bytes of pixel k (0..7) from the lane's 24 texture bytes t[0..5].
+__device__ inline uint32_t bgr_of(const uint32_t (&t)[6], int k) {
+  const int b = 3 * k, w = b >> 2, s = 8 * (b & 3);
+  const uint64_t pair = uint64_t(t[w]) | (uint64_t(w + 1 < 6 ? t[w + 1] : 0u) << 32);
+  return uint32_t(pair >> s) & 0xffffffu;
+}
+
+// Block-wide exclusive scan of one int per lane: (exclusive prefix, block total).
+__device__ inline int2 block_scan(int x, int* s_wtot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_wtot[wave] = incl;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / 64; ++w) {
+    off += w < wave ? s_wtot[w] : 0;
+    tot += s_wtot[w];
+  }
+  return make_int2(off + incl - x, tot);
 }
 
 template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS>
-__global__ __launch_bounds__(kBlock) void main2_kernel(MainParams p) {
+__global__ __launch_bounds__(kBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) void main3_kernel(Main3Params P) {
   using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
   constexpr int NS = ROW_MODE == 2 ? 2 : 1;
-  __shared__ uint32_t s_code[kTilePx];     // valid item m: col | row << 16; phase C: keep/map
-  __shared__ uint16_t s_off[kTilePx];      // pixel offset inside the tile
-  __shared__ uint8_t s_tex[kTilePx * 3];   // the tile's BGR bytes (raw pixel order)
-  __shared__ XT s_xyz[NS][kTilePx * 3];
-  __shared__ int s_tot4[4];
-  __shared__ uint64_t s_excl;
-  uint8_t* s_keep = reinterpret_cast<uint8_t*>(s_code);                 // aliases after phase B
-  uint16_t* s_map = reinterpret_cast<uint16_t*>(s_code) + kTilePx;
+  constexpr int kIt = kTilePx / kBlock;    // 8 item rounds of 256 at most
+  __shared__ uint32_t s_code[kTilePx];     // valid item: col | row << 16
+  __shared__ uint32_t s_bgr[kTilePx];      // its BGR (24 bits)
+  __shared__ uint16_t s_off[kTilePx];      // its pixel offset inside the tile
+  __shared__ int s_wtot[kBlock / 64];
+  __shared__ int s_cnt[NS][kIt][kBlock / 64];   // kept points per (round, wave)
+  __shared__ uint64_t s_excl[NS];
 
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  const int tile = int(blockIdx.x);        // static ids: the look-back helper guarantees progress
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles = int(P.c.n_tiles);
+  const int view = int(blockIdx.x) / tiles;          // grid = views x tiles, view-major
+  const int tile = int(blockIdx.x) - view * tiles;
+  const MainParams p = view_params(P, view);
   const int64_t tile_px = int64_t(tile) * kTilePx;
   const int64_t px0 = tile_px + int64_t(tid) * kPx;
-  const bool tail = tile == p.n_tiles - 1;           // wave-uniform: guarded reads only here
+  const bool tail = tile == tiles - 1;               // block-uniform: guarded reads only here
 
-  // ------------------------------------------------------------ phase A: decode 8 pixels
+  // ------------------------------------------------------------ A: decode + tile compaction
+  int n_items;
   {
-    const int64_t tb = px0 * 3;            // texture of the tile, coalesced
-    uint32_t* st32 = reinterpret_cast<uint32_t*>(s_tex);
+    uint32_t tex[6] = {0, 0, 0, 0, 0, 0};
     if (!tail) {
-      const uint2* tq = reinterpret_cast<const uint2*>(p.texture + tb);
+      const uint2* tq = reinterpret_cast<const uint2*>(p.texture + px0 * 3);
       const uint2 t0 = tq[0], t1 = tq[1], t2 = tq[2];
-      st32[6 * tid + 0] = t0.x; st32[6 * tid + 1] = t0.y; st32[6 * tid + 2] = t1.x;
-      st32[6 * tid + 3] = t1.y; st32[6 * tid + 4] = t2.x; st32[6 * tid + 5] = t2.y;
+      tex[0] = t0.x; tex[1] = t0.y; tex[2] = t1.x; tex[3] = t1.y; tex[4] = t2.x; tex[5] = t2.y;
     } else {
       for (int k = 0; k < 3 * kPx; ++k)
-        s_tex[24 * tid + k] = tb + k < p.n_px * 3 ? p.texture[tb + k] : 0;
+        if (px0 * 3 + k < p.n_px * 3) tex[k >> 2] |= uint32_t(p.texture[px0 * 3 + k]) << (8 * (k & 3));
     }
-  }
-  uint32_t valid;
-  int col[kPx], row[kPx];
-  decode_lane<ROW_MODE, SRC_FRAMES, 8>(p, px0, tail, valid, col, row);
-  const int2 vs = block_scan(__popc(valid), s_tot4);
-  const int n_items = vs.y;
-  {
-    int m = vs.x;
+    uint32_t valid;
+    int col[kPx], row[kPx];
+    decode_lane<ROW_MODE, SRC_FRAMES, 8>(p, px0, tail, valid, col, row);
+    const int2 sc = block_scan(__popc(valid), s_wtot);
+    n_items = sc.y;
+    int m = sc.x;
 #pragma unroll
     for (int k = 0; k < kPx; ++k)
       if (valid & (1u << k)) {
         s_code[m] = pack_code<ROW_MODE>(p, col[k], row[k]);
+        s_bgr[m] = bgr_of(tex, k);
         s_off[m] = uint16_t(tid * kPx + k);
         ++m;
       }
   }
   __syncthreads();
 
-  // ------------------------------------------------------------ phase B: triangulate items
+  // ------------------------------------------------------------ B: triangulate, balanced
+  // Item m = tid + 256 * i: every wave gets a quarter of the tile's valid pixels.
   const int v0 = int(tile_px / p.width);
   const int u0 = int(tile_px - int64_t(v0) * p.width);
-  uint32_t keepbits = 0;                   // 2 bits per owned item m = tid + 256*i
-#pragma unroll 2
-  for (int i = 0; i < kTilePx / kBlock; ++i) {
-    const int m = tid + kBlock * i;
-    if (m < n_items) {
-      const uint32_t code = s_code[m];
-      int u = u0 + int(s_off[m]), v = v0;
+  XT pts[NS][kIt][3];
+  uint64_t km[NS][kIt];
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) km[s][i] = 0;
+    if (i * kBlock < n_items) {                      // block-uniform
+      const int m = tid + kBlock * i;
+      const bool in = m < n_items;
+      const uint32_t code = in ? s_code[m] : 0u;
+      int u = u0 + (in ? int(s_off[m]) : 0), v = v0;
       while (u >= p.width) { u -= p.width; ++v; }
       uint32_t keep;
-      if (p.dbg & 2) {
-        keep = ROW_MODE == 2 ? 3 : 1;
-        s_xyz[0][3 * m] = XT(code & 0xffff); s_xyz[0][3 * m + 1] = XT(code >> 16); s_xyz[0][3 * m + 2] = XT(u);
-        if constexpr (ROW_MODE == 2) { s_xyz[NS - 1][3 * m] = XT(v); s_xyz[NS - 1][3 * m + 1] = 0; s_xyz[NS - 1][3 * m + 2] = 0; }
+      if (p.dbg & 2) {                               // ablation: trivial triangulation
+        keep = in ? (ROW_MODE == 2 ? 3u : 1u) : 0u;
+        pts[0][i][0] = XT(code & 0xffff); pts[0][i][1] = XT(code >> 16); pts[0][i][2] = XT(u);
+        if constexpr (ROW_MODE == 2) { pts[NS - 1][i][0] = XT(v); pts[NS - 1][i][1] = 0; pts[NS - 1][i][2] = 0; }
       } else {
         const TriOut o = tri_item<ROW_MODE, RAYS>(p, code, u, v);
-        keep = o.keep;
-        s_xyz[0][3 * m] = XT(o.x); s_xyz[0][3 * m + 1] = XT(o.y); s_xyz[0][3 * m + 2] = XT(o.z);
-        if constexpr (ROW_MODE == 2) {
-          s_xyz[NS - 1][3 * m] = XT(o.rx); s_xyz[NS - 1][3 * m + 1] = XT(o.ry); s_xyz[NS - 1][3 * m + 2] = XT(o.rz);
-        }
+        keep = in ? o.keep : 0u;
+        pts[0][i][0] = XT(o.x); pts[0][i][1] = XT(o.y); pts[0][i][2] = XT(o.z);
+        if constexpr (ROW_MODE == 2) { pts[NS - 1][i][0] = XT(o.rx); pts[NS - 1][i][1] = XT(o.ry); pts[NS - 1][i][2] = XT(o.rz); }
       }
-      keepbits |= keep << (2 * i);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) km[s][i] = __ballot((keep >> s) & 1u);
     }
-  }
-  __syncthreads();                                   // s_code no longer needed
-  for (int i = 0; i < kTilePx / kBlock; ++i) {
-    const int m = tid + kBlock * i;
-    if (m < n_items) s_keep[m] = uint8_t((keepbits >> (2 * i)) & 3u);
+    if (lane == 0) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) s_cnt[s][i][wave] = __popcll(km[s][i]);
+    }
   }
   __syncthreads();
 
-  // ------------------------------------------------------------ phase C: ordered output
+  // ------------------------------------------------------------ C: tile offset (look-back)
+  if (wave == 0) {
 #pragma unroll 1
-  for (int stream = 0; stream < NS; ++stream) {
-    const int m0 = tid * kPx;
-    uint32_t kb = 0;
-#pragma unroll
-    for (int k = 0; k < kPx; ++k)
-      if (m0 + k < n_items) kb |= uint32_t((s_keep[m0 + k] >> stream) & 1u) << k;
-    const int2 ks = block_scan(__popc(kb), s_tot4);
-    const int agg = ks.y;
-    {
-      int q = ks.x;
-#pragma unroll
-      for (int k = 0; k < kPx; ++k)
-        if (kb & (1u << k)) s_map[q++] = uint16_t(m0 + k);
-    }
-    uint64_t* st = p.states + int64_t(stream) * p.n_tiles;
-    if (wave == 0) {
-      const uint64_t excl = lookback_prefix<ROW_MODE, SRC_FRAMES, RAYS>(p, st, tile, agg, stream);
-      if ((tid & 63) == 0) {
-        s_excl = excl;
-        if (tile == p.n_tiles - 1) {
-          p.ws->totals[stream] = int64_t(excl) + agg;
+    for (int s = 0; s < NS; ++s) {
+      int agg = 0;
+      for (int q = 0; q < kIt * (kBlock / 64); ++q) agg += (&s_cnt[s][0][0])[q];
+      uint64_t* st = p.states + int64_t(s) * tiles;
+      uint64_t excl;
+      int ht;
+      while (!lookback_try(p, st, tile, agg, excl, ht)) {
+        // a predecessor has not published for long (it may not be dispatched yet): publish
+        // its aggregate for it, computed by this wave, and look back again
+        const int hagg = tile_keep_count_wave<ROW_MODE, SRC_FRAMES, RAYS>(p, ht, s);
+        if (lane == 0) {
+          publish_agg(&st[ht], hagg);
+          atomicOr(&p.ws->error, 2u);                // diagnostic: a helper ran (not an error)
+        }
+      }
+      if (lane == 0) {
+        s_excl[s] = excl;
+        if (tail) {
+          p.ws->totals[s] = int64_t(excl) + agg;
           if (ROW_MODE != 2) *p.count = int64_t(excl) + agg;
         }
       }
     }
-    __syncthreads();
-    if (!(p.dbg & 4)) {
-      const int64_t base = int64_t(s_excl);
-      const XT* sx = s_xyz[stream];
-      XT* gx = reinterpret_cast<XT*>(stream == 0 ? p.xyz : p.scratch_xyz) + base * 3;
-      for (int i = tid; i < agg * 3; i += kBlock) {
-        const int q = i / 3;
-        gx[i] = sx[3 * int(s_map[q]) + (i - 3 * q)];
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------ D: ordered stores from registers
+  if (p.dbg & 4) return;                             // ablation: no output stores
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int64_t base = int64_t(s_excl[s]);
+    XT* gx = reinterpret_cast<XT*>(s == 0 ? p.xyz : p.scratch_xyz);
+    uint8_t* gb = s == 0 ? p.bgr : p.scratch_bgr;
+#pragma unroll
+    for (int i = 0; i < kIt; ++i) {
+      int before = 0, round = 0;
+#pragma unroll
+      for (int w = 0; w < kBlock / 64; ++w) {
+        const int c = s_cnt[s][i][w];
+        before += w < wave ? c : 0;
+        round += c;
       }
-      uint8_t* gb = (stream == 0 ? p.bgr : p.scratch_bgr);
-      const int64_t lo = base * 3, hi = (base + agg) * 3;
-      const int64_t lo4 = (lo + 3) & ~int64_t(3), hi4 = hi & ~int64_t(3);
-      auto byte_at = [&](int64_t b) -> uint32_t {   // b: byte offset inside the tile's BGR run
-        const int q = int(b / 3);
-        return s_tex[3 * int(s_off[s_map[q]]) + int(b - 3 * q)];
-      };
-      if (lo4 < hi4) {
-        for (int64_t i = lo4 + 4 * int64_t(tid); i < hi4; i += 4 * kBlock) {
-          const int64_t b = i - lo;
-          *reinterpret_cast<uint32_t*>(gb + i) =
-              byte_at(b) | (byte_at(b + 1) << 8) | (byte_at(b + 2) << 16) | (byte_at(b + 3) << 24);
-        }
-        if (tid < lo4 - lo) gb[lo + tid] = uint8_t(byte_at(tid));
-        if (tid < hi - hi4) gb[hi4 + tid] = uint8_t(byte_at(hi4 - lo + tid));
-      } else {
-        for (int64_t i = lo + tid; i < hi; i += kBlock) gb[i] = uint8_t(byte_at(i - lo));
+      if ((km[s][i] >> lane) & 1ull) {
+        const int64_t q = base + before + __popcll(km[s][i] & lt);
+        gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
+        const uint32_t c = s_bgr[tid + kBlock * i];
+        gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
       }
+      base += round;
     }
-    __syncthreads();
   }
 }
 
@@ -1252,7 +1024,9 @@ struct Plan {
 
 // Which frames each axis reads and how the code is shifted (processing.py:80-122,
 // sl_system.py:546-585).
-int make_plan(const slg_capture* cap, const slg_decode_params* dp, Plan* pl) {
+int make_plan(const slg_capture* cap, const slg_decode_params* dp, Plan* out) {   // out may be NULL
+  Plan tmp;
+  Plan* pl = out ? out : &tmp;
   if (cap->n_frames < 4)
     return fail(SLG_ERR_NOT_ENOUGH, "Not enough images (got %d, need at least 4).", cap->n_frames);
   if (dp->proj_cols < 1 || dp->proj_rows < 1) return fail(SLG_ERR_INVALID, "projector size must be positive");
@@ -1311,15 +1085,13 @@ int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* black
     sp.wsv[v] = reinterpret_cast<WsHeader*>(workspace + int64_t(v) * ws_stride);
   }
   sp.n_px = n_px;
-  sp.n_state_words = 2 * n_tiles_of(n_px);
+  sp.n_state_words = n_state_words(n_px);
   sp.thresh_mode = dp ? dp->thresh_mode : SLG_THRESH_MANUAL;
   sp.shadow_val = dp ? dp->shadow_val : 0.0;
   sp.contrast_val = dp ? dp->contrast_val : 0.0;
   sp.dbg = debug_flags();
-  const int64_t chunks = (n_px + kPx - 1) / kPx;
-  int64_t grid = (chunks + kBlock - 1) / kBlock;
-  const int64_t cap = n_views > 1 ? 256 : 512;
-  if (grid > cap) grid = cap;
+  int64_t grid = (n_px + int64_t(kBlock) * kStatsPx - 1) / (int64_t(kBlock) * kStatsPx);
+  if (grid > 1024) grid = 1024;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(stats_kernel, dim3(unsigned(grid), unsigned(n_views)), dim3(kBlock), 0, s, sp);
   return check_launch("stats_kernel");
@@ -1328,29 +1100,6 @@ int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* black
 int stats_launch(const uint8_t* white, const uint8_t* black, int64_t n_px, const slg_decode_params* dp,
                  void* workspace, hipStream_t s) {
   return stats_launch_batch(&white, &black, 1, n_px, dp, static_cast<char*>(workspace), 0, s);
-}
-
-using MainFn = void (*)(MainParams);
-
-int kernel_select() {   // profiling A/B only: SLG_MAIN=1 selects the first-generation kernel
-  const char* e = getenv("SLG_MAIN");
-  return e ? atoi(e) : 2;
-}
-
-template <int RM, int X64, int SRC, int WM, int RAYS>
-MainFn pick5() {
-  if (kernel_select() == 1) return main_kernel<RM, X64, SRC, WM, 1, RAYS>;
-  return main2_kernel<RM, X64, SRC, RAYS>;
-}
-
-template <int SRC, int WM>
-MainFn pick_tri(int row_mode, int x64, int rays) {
-#define SLG_CASE(RM, X, R) if (row_mode == RM && x64 == X && rays == R) return pick5<RM, X, SRC, WM, R>();
-  SLG_CASE(0, 0, 0) SLG_CASE(0, 0, 1) SLG_CASE(0, 1, 0) SLG_CASE(0, 1, 1)
-  SLG_CASE(1, 0, 0) SLG_CASE(1, 0, 1) SLG_CASE(1, 1, 0) SLG_CASE(1, 1, 1)
-  SLG_CASE(2, 0, 0) SLG_CASE(2, 0, 1) SLG_CASE(2, 1, 0) SLG_CASE(2, 1, 1)
-#undef SLG_CASE
-  return nullptr;
 }
 
 int fill_calib(MainParams& mp, const slg_calib* c, const slg_tri_params* tp, int64_t n_px, int width) {
@@ -1393,21 +1142,135 @@ int debug_flags() {   // profiling ablations only; unset in production
   return e ? atoi(e) : 0;
 }
 
-int launch_main(MainFn fn, MainParams mp, const slg_tri_params* tp, const slg_cloud* out, hipStream_t s) {
-  if (!fn) return fail(SLG_ERR_INVALID, "no kernel for this configuration");
-  mp.dbg = debug_flags();
-  hipLaunchKernelGGL(fn, dim3(unsigned(mp.n_tiles)), dim3(kBlock), 0, s, mp);
-  int rc = check_launch("main_kernel");
+using Main3Fn = void (*)(Main3Params);
+
+template <int SRC>
+Main3Fn pick_main(int row_mode, int x64, int rays) {
+#define SLG_CASE(RM, X, R) if (row_mode == RM && x64 == X && rays == R) return main3_kernel<RM, X, SRC, R>;
+  SLG_CASE(0, 0, 0) SLG_CASE(0, 0, 1) SLG_CASE(0, 1, 0) SLG_CASE(0, 1, 1)
+  SLG_CASE(1, 0, 0) SLG_CASE(1, 0, 1) SLG_CASE(1, 1, 0) SLG_CASE(1, 1, 1)
+  SLG_CASE(2, 0, 0) SLG_CASE(2, 0, 1) SLG_CASE(2, 1, 0) SLG_CASE(2, 1, 1)
+#undef SLG_CASE
+  return nullptr;
+}
+
+// Output + workspace pointers of one view (the per-view half of fill_out).
+int fill_view(ViewIO& io, const slg_cloud* out, const slg_tri_params* tp, int64_t n_px, void* ws) {
+  MainParams mp{};
+  const int rc = fill_out(mp, out, tp, n_px, ws);
   if (rc) return rc;
-  if (tp && tp->row_mode == 2) {
-    const unsigned grid = unsigned((mp.n_px + kBlock - 1) / kBlock);
+  io.xyz = mp.xyz; io.bgr = mp.bgr; io.count = mp.count; io.ws = mp.ws; io.states = mp.states;
+  io.scratch_xyz = mp.scratch_xyz; io.scratch_bgr = mp.scratch_bgr;
+  return SLG_OK;
+}
+
+// One main3 launch over mp.n_views views (<= kMaxViews), then the row_mode-2 tails.
+int launch_main3(Main3Fn fn, Main3Params& mp, const slg_tri_params* tp, const slg_cloud* outs, hipStream_t s) {
+  if (!fn) return fail(SLG_ERR_INVALID, "no kernel for this configuration");
+  mp.c.dbg = debug_flags();
+  const int64_t grid = mp.c.n_tiles * mp.n_views;
+  if (grid > INT_MAX) return fail(SLG_ERR_UNSUPPORTED, "batch too large for one launch");
+  hipLaunchKernelGGL(fn, dim3(unsigned(grid)), dim3(kBlock), 0, s, mp);
+  int rc = check_launch("main kernel");
+  if (rc || !tp || tp->row_mode != 2) return rc;
+  const unsigned tg = unsigned((mp.c.n_px + kBlock - 1) / kBlock);
+  for (int v = 0; v < mp.n_views; ++v) {
+    const ViewIO& io = mp.v[v];
     if (tp->xyz_f64)
-      hipLaunchKernelGGL(row_tail_kernel<1>, dim3(grid), dim3(kBlock), 0, s, mp.ws, mp.scratch_xyz, mp.scratch_bgr, out->xyz, out->bgr, out->count);
+      hipLaunchKernelGGL(row_tail_kernel<1>, dim3(tg), dim3(kBlock), 0, s, io.ws, io.scratch_xyz, io.scratch_bgr, outs[v].xyz, outs[v].bgr, outs[v].count);
     else
-      hipLaunchKernelGGL(row_tail_kernel<0>, dim3(grid), dim3(kBlock), 0, s, mp.ws, mp.scratch_xyz, mp.scratch_bgr, out->xyz, out->bgr, out->count);
+      hipLaunchKernelGGL(row_tail_kernel<0>, dim3(tg), dim3(kBlock), 0, s, io.ws, io.scratch_xyz, io.scratch_bgr, outs[v].xyz, outs[v].bgr, outs[v].count);
     rc = check_launch("row_tail_kernel");
+    if (rc) return rc;
   }
-  return rc;
+  return SLG_OK;
+}
+
+// Views of one batch must share the launch-wide parameters.
+int check_batch(const slg_capture* caps, int n_views) {
+  for (int v = 0; v < n_views; ++v) {
+    const int rc = check_capture(&caps[v]);
+    if (rc) return rc;
+    if (!caps[v].texture) return fail(SLG_ERR_INVALID, "capture %d: texture is NULL", v);
+    if (reinterpret_cast<uintptr_t>(caps[v].texture) & 7) return fail(SLG_ERR_INVALID, "texture must be 8-byte aligned");
+    if (caps[v].height != caps[0].height || caps[v].width != caps[0].width)
+      return fail(SLG_ERR_INVALID, "all views of a batch must share one geometry");
+  }
+  return SLG_OK;
+}
+
+// Fused decode + triangulate of n_views views (thresholds already in each view's workspace
+// slice): one main3 launch per kMaxViews views.  timing_events: 2 per launch, or NULL.
+int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* dp, const slg_calib* calib,
+                const slg_tri_params* tp, char* ws, int64_t ws_stride, const slg_cloud* outs,
+                void* const* timing_events, hipStream_t s) {
+  if (!caps || n_views < 1 || !dp || !ws || !outs) return fail(SLG_ERR_INVALID, "NULL argument");
+  int rc = check_batch(caps, n_views);
+  if (rc) return rc;
+  for (int v = 0; v < n_views; ++v) {
+    rc = make_plan(&caps[v], dp, nullptr);
+    if (rc) return rc;
+  }
+  const int64_t n_px = int64_t(caps[0].height) * caps[0].width;
+  if (n_views > 1 && (ws_stride < ws_total(n_px) || (ws_stride & 255)))
+    return fail(SLG_ERR_INVALID, "ws_stride too small or not 256-aligned");
+  Main3Params mp{};
+  rc = fill_calib(mp.c, calib, tp, n_px, caps[0].width);
+  if (rc) return rc;
+  mp.c.n_tiles = n_tiles_of(n_px);
+  const Main3Fn fn = pick_main<1>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode);
+  for (int v0 = 0, launch = 0; v0 < n_views; v0 += kMaxViews, ++launch) {
+    mp.n_views = n_views - v0 < kMaxViews ? n_views - v0 : kMaxViews;
+    for (int k = 0; k < mp.n_views; ++k) {
+      const int v = v0 + k;
+      ViewIO& io = mp.v[k];
+      io = ViewIO{};
+      rc = fill_view(io, &outs[v], tp, n_px, ws + int64_t(v) * ws_stride);
+      if (rc) return rc;
+      io.frames = caps[v].frames;
+      io.texture = caps[v].texture;
+      io.stride = caps[v].frame_stride;
+      Plan pl;
+      make_plan(&caps[v], dp, &pl);
+      io.col_first = pl.col_first; io.col_pairs = pl.col_pairs; io.col_pre = pl.col_pre; io.col_post = pl.col_post;
+      io.row_first = pl.row_first; io.row_pairs = pl.row_pairs; io.row_pre = pl.row_pre; io.row_post = pl.row_post;
+    }
+    if (timing_events && timing_events[2 * launch]) hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * launch]), s);
+    rc = launch_main3(fn, mp, tp, &outs[v0], s);
+    if (rc) return rc;
+    if (timing_events && timing_events[2 * launch + 1]) hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * launch + 1]), s);
+  }
+  return SLG_OK;
+}
+
+// Stats of n_views views (one launch per kMaxBatch views).
+int stats_batch(const slg_capture* caps, int n_views, const slg_decode_params* dp, char* ws, int64_t ws_stride,
+                hipStream_t s) {
+  if (!caps || n_views < 1 || !dp || !ws) return fail(SLG_ERR_INVALID, "NULL argument");
+  if (dp->thresh_mode < 0 || dp->thresh_mode > 2) return fail(SLG_ERR_INVALID, "bad thresh_mode");
+  for (int v = 0; v < n_views; ++v) {
+    const int rc = check_capture(&caps[v]);
+    if (rc) return rc;
+    if (caps[v].n_frames < 4)
+      return fail(SLG_ERR_NOT_ENOUGH, "Not enough images (got %d, need at least 4).", caps[v].n_frames);
+    if (caps[v].height != caps[0].height || caps[v].width != caps[0].width)
+      return fail(SLG_ERR_INVALID, "all views of a batch must share one geometry");
+  }
+  const int64_t n_px = int64_t(caps[0].height) * caps[0].width;
+  if (n_views > 1 && (ws_stride < ws_total(n_px) || (ws_stride & 255)))
+    return fail(SLG_ERR_INVALID, "ws_stride too small or not 256-aligned");
+  for (int v0 = 0; v0 < n_views; v0 += kMaxBatch) {
+    const int nb = n_views - v0 < kMaxBatch ? n_views - v0 : kMaxBatch;
+    const uint8_t* wh[kMaxBatch];
+    const uint8_t* bl[kMaxBatch];
+    for (int v = 0; v < nb; ++v) {
+      wh[v] = caps[v0 + v].frames;
+      bl[v] = caps[v0 + v].frames + caps[v0 + v].frame_stride;
+    }
+    const int rc = stats_launch_batch(wh, bl, nb, n_px, dp, ws + int64_t(v0) * ws_stride, ws_stride, s);
+    if (rc) return rc;
+  }
+  return SLG_OK;
 }
 
 // ------------------------------------------------------------------ ASCII PLY (host)
@@ -1514,9 +1377,9 @@ int32_t slg_decode(const slg_capture* cap, const slg_decode_params* dp, void* wo
   mp.out_col = col_out; mp.out_row = row_out; mp.out_mask = mask_out;
   mp.ws = reinterpret_cast<WsHeader*>(workspace);
   mp.n_tiles = n_tiles_of(n_px);
-  hipLaunchKernelGGL((main_kernel<0, 0, 1, 1, 0, 0>), dim3(unsigned(mp.n_tiles)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(decode_maps_kernel, dim3(unsigned(mp.n_tiles)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), mp);
-  return check_launch("decode main_kernel");
+  return check_launch("decode_maps_kernel");
 }
 
 int32_t slg_triangulate(const slg_maps* maps, const slg_calib* calib, const slg_tri_params* tp, void* workspace,
@@ -1537,36 +1400,28 @@ int32_t slg_triangulate(const slg_maps* maps, const slg_calib* calib, const slg_
   hipStream_t s = static_cast<hipStream_t>(stream);
   rc = stats_launch(nullptr, nullptr, n_px, nullptr, workspace, s);   // arms states only (manual mode)
   if (rc) return rc;
-  return launch_main(pick_tri<0, 0>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode), mp, tp, out, s);
+  Main3Params m3{};
+  m3.c = mp;
+  m3.n_views = 1;
+  rc = fill_view(m3.v[0], out, tp, n_px, workspace);
+  if (rc) return rc;
+  m3.v[0].in_col = maps->col; m3.v[0].in_row = maps->row; m3.v[0].in_mask = maps->mask;
+  m3.v[0].texture = maps->texture;
+  return launch_main3(pick_main<0>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode), m3, tp, out, s);
 }
 
 static int reconstruct_impl(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,
                             const slg_tri_params* tp, void* workspace, const slg_cloud* out, void* stream,
                             bool with_stats) {
-  int rc = check_capture(cap);
-  if (rc) return rc;
-  if (!dp || !workspace || !cap->texture) return fail(SLG_ERR_INVALID, "NULL argument");
-  if (reinterpret_cast<uintptr_t>(cap->texture) & 7) return fail(SLG_ERR_INVALID, "texture must be 8-byte aligned");
-  Plan pl;
-  rc = make_plan(cap, dp, &pl);
-  if (rc) return rc;
-  const int64_t n_px = int64_t(cap->height) * cap->width;
-  MainParams mp{};
-  rc = fill_calib(mp, calib, tp, n_px, cap->width);
-  if (rc) return rc;
-  rc = fill_out(mp, out, tp, n_px, workspace);
-  if (rc) return rc;
-  mp.frames = cap->frames;
-  mp.stride = cap->frame_stride;
-  mp.texture = cap->texture;
-  mp.col_first = pl.col_first; mp.col_pairs = pl.col_pairs; mp.col_pre = pl.col_pre; mp.col_post = pl.col_post;
-  mp.row_first = pl.row_first; mp.row_pairs = pl.row_pairs; mp.row_pre = pl.row_pre; mp.row_post = pl.row_post;
+  if (!cap || !dp || !workspace) return fail(SLG_ERR_INVALID, "NULL argument");
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (with_stats) {
-    rc = stats_launch(cap->frames, cap->frames + cap->frame_stride, n_px, dp, workspace, s);
+    int rc = check_batch(cap, 1);
+    if (!rc) rc = make_plan(cap, dp, nullptr);
+    if (!rc) rc = stats_batch(cap, 1, dp, static_cast<char*>(workspace), 0, s);
     if (rc) return rc;
   }
-  return launch_main(pick_tri<1, 0>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode), mp, tp, out, s);
+  return fused_batch(cap, 1, dp, calib, tp, static_cast<char*>(workspace), 0, out, nullptr, s);
 }
 
 int32_t slg_reconstruct(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,
@@ -1617,34 +1472,33 @@ int32_t slg_reconstruct_batch(const slg_capture* caps, int32_t n_views, const sl
                               int64_t ws_stride, const slg_cloud* outs, void* const* timing_events,
                               void* stream) {
   if (!caps || n_views < 1 || !dp || !workspace || !outs) return fail(SLG_ERR_INVALID, "NULL argument");
-  const int64_t n_px = int64_t(caps[0].height) * caps[0].width;
-  if (ws_stride < ws_total(n_px) || (ws_stride & 255)) return fail(SLG_ERR_INVALID, "ws_stride too small or not 256-aligned");
-  for (int v = 0; v < n_views; ++v) {
-    int rc = check_capture(&caps[v]);
-    if (rc) return rc;
-    if (caps[v].height != caps[0].height || caps[v].width != caps[0].width)
-      return fail(SLG_ERR_INVALID, "all views of a batch must share one geometry");
-  }
   hipStream_t s = static_cast<hipStream_t>(stream);
   char* ws = static_cast<char*>(workspace);
-  for (int v0 = 0; v0 < n_views; v0 += kMaxBatch) {
-    const int nb = n_views - v0 < kMaxBatch ? n_views - v0 : kMaxBatch;
-    const uint8_t* wh[kMaxBatch];
-    const uint8_t* bl[kMaxBatch];
-    for (int v = 0; v < nb; ++v) {
-      wh[v] = caps[v0 + v].frames;
-      bl[v] = caps[v0 + v].frames + caps[v0 + v].frame_stride;
-    }
-    int rc = stats_launch_batch(wh, bl, nb, n_px, dp, ws + int64_t(v0) * ws_stride, ws_stride, s);
+  int rc = check_batch(caps, n_views);              // validate everything before enqueueing
+  for (int v = 0; v < n_views && !rc; ++v) rc = make_plan(&caps[v], dp, nullptr);
+  if (rc) return rc;
+  for (int v0 = 0, launch = 0; v0 < n_views; v0 += kMaxViews, ++launch) {
+    const int nb = n_views - v0 < kMaxViews ? n_views - v0 : kMaxViews;
+    rc = stats_batch(caps + v0, nb, dp, ws + int64_t(v0) * ws_stride, ws_stride, s);
     if (rc) return rc;
-    for (int v = v0; v < v0 + nb; ++v) {
-      if (timing_events && timing_events[2 * v]) hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * v]), s);
-      rc = reconstruct_impl(&caps[v], dp, calib, tp, ws + int64_t(v) * ws_stride, &outs[v], stream, false);
-      if (rc) return rc;
-      if (timing_events && timing_events[2 * v + 1]) hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * v + 1]), s);
-    }
+    rc = fused_batch(caps + v0, nb, dp, calib, tp, ws + int64_t(v0) * ws_stride, ws_stride, outs + v0,
+                     timing_events ? timing_events + 2 * launch : nullptr, s);
+    if (rc) return rc;
   }
   return SLG_OK;
+}
+
+int32_t slg_decode_stats_batch(const slg_capture* caps, int32_t n_views, const slg_decode_params* dp,
+                               void* workspace, int64_t ws_stride, void* stream) {
+  return stats_batch(caps, n_views, dp, static_cast<char*>(workspace), ws_stride, static_cast<hipStream_t>(stream));
+}
+
+int32_t slg_decode_triangulate_batch(const slg_capture* caps, int32_t n_views, const slg_decode_params* dp,
+                                     const slg_calib* calib, const slg_tri_params* tp, void* workspace,
+                                     int64_t ws_stride, const slg_cloud* outs, void* const* timing_events,
+                                     void* stream) {
+  return fused_batch(caps, n_views, dp, calib, tp, static_cast<char*>(workspace), ws_stride, outs, timing_events,
+                     static_cast<hipStream_t>(stream));
 }
 
 int32_t slg_rays_match_pinhole(const double* rays, int32_t height, int32_t width, double fx, double fy, double cx,

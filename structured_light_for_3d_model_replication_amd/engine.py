@@ -286,37 +286,116 @@ class Reconstructor:
         return int(np.frombuffer(hdr[3 * 256 * 4 + 12: 3 * 256 * 4 + 16].tobytes(), np.uint32)[0])
 
 
-class BatchReconstructor:
-    """Many views of one geometry per call (``slg_reconstruct_batch``): one batched stats
-    launch, then the fused kernels back to back on one stream.  Owns ``max_views`` workspace
-    slices; ``run`` only enqueues (no host sync)."""
+MAX_VIEWS_PER_LAUNCH = 16     # kMaxViews in csrc/slgpu.hip
 
-    def __init__(self, height: int, width: int, max_views: int, device=None):
+
+@dataclass
+class PreparedBatch:
+    """ctypes argument arrays of one batch, bound to one workspace slot."""
+    caps: object
+    n: int
+    dp: object
+    calib: object
+    tp: object
+    clouds: object
+    slot: int
+
+    @property
+    def n_launches(self) -> int:
+        return (self.n + MAX_VIEWS_PER_LAUNCH - 1) // MAX_VIEWS_PER_LAUNCH
+
+
+class BatchReconstructor:
+    """Many views of one geometry per call (``process_multi_ply(mode='batch')``,
+    server/processing.py:314-334): per group of up to 16 views one batched stats launch and ONE
+    fused decode+triangulate launch over all of them.
+
+    Owns ``slots`` workspace sets of ``max_views`` slices each, so the stats of batch k+1 can run
+    on a side stream while batch k's fused launch runs (:meth:`run_pipelined`).  Every method
+    only enqueues work (no host sync)."""
+
+    def __init__(self, height: int, width: int, max_views: int, device=None, slots: int = 2):
         self.device = device or default_device()
         self.height, self.width, self.n_px = int(height), int(width), int(height) * int(width)
-        self.max_views = int(max_views)
+        self.max_views, self.slots = int(max_views), int(slots)
         one = int(N.lib().slg_workspace_bytes(self.n_px))
         self.ws_stride = (one + 255) // 256 * 256
-        self.workspace = torch.empty(self.ws_stride * self.max_views, dtype=torch.uint8, device=self.device)
-        for v in range(self.max_views):
+        self.workspace = torch.empty(self.ws_stride * self.max_views * self.slots, dtype=torch.uint8,
+                                     device=self.device)
+        for v in range(self.max_views * self.slots):
             N.check(N.lib().slg_workspace_init(ctypes.c_void_p(self.workspace.data_ptr() + v * self.ws_stride),
                                                self.ws_stride, _stream()))
+        self._events = []
 
-    def prepare(self, frames, cfg: DecodeConfig, calib: DeviceCalib, outs, row_mode=1, epipolar_tol=2.0):
+    def _ws(self, slot: int) -> ctypes.c_void_p:
+        return ctypes.c_void_p(self.workspace.data_ptr() + slot * self.max_views * self.ws_stride)
+
+    def header(self, slot: int, view: int) -> torch.Tensor:
+        """Workspace header (thresholds, flags) of one view slice."""
+        off = (slot * self.max_views + view) * self.ws_stride
+        return self.workspace[off: off + 8192]
+
+    def prepare(self, frames, cfg: DecodeConfig, calib: DeviceCalib, outs, row_mode=1, epipolar_tol=2.0,
+                slot: int = 0) -> PreparedBatch:
         """Build the argument arrays once (lets a hot loop re-issue the same batch cheaply)."""
         n = len(frames)
-        if n > self.max_views or len(outs) != n:
-            raise ValueError("batch larger than the engine or outputs/frames mismatch")
+        if n > self.max_views or len(outs) != n or not 0 <= slot < self.slots:
+            raise ValueError("batch larger than the engine, outputs/frames mismatch, or bad slot")
+        for f in frames:
+            self_geom = (f.height, f.width)
+            if self_geom != (self.height, self.width):
+                raise ValueError(f"engine built for {self.width}x{self.height}, got {f.width}x{f.height}")
         caps = (N.Capture * n)(*[f.capture() for f in frames])
         clouds = (N.Cloud * n)(*[o.struct() for o in outs])
-        return (caps, n, cfg.struct(), calib.struct(),
-                N.TriParams(int(row_mode), int(outs[0].xyz_f64), float(epipolar_tol)), clouds)
+        return PreparedBatch(caps, n, cfg.struct(), calib.struct(),
+                             N.TriParams(int(row_mode), int(outs[0].xyz_f64), float(epipolar_tol)),
+                             clouds, slot)
 
-    def run(self, prepared, events=None, stream=None):
-        caps, n, dp, c, tp, clouds = prepared
-        ev = None
-        if events is not None:
-            ev = (ctypes.c_void_p * (2 * n))(*[int(e) if e else None for e in events])
-        N.check(N.lib().slg_reconstruct_batch(caps, n, ctypes.byref(dp), ctypes.byref(c), ctypes.byref(tp),
-                                              _vp(self.workspace), self.ws_stride, clouds, ev,
-                                              _stream(stream)))
+    @staticmethod
+    def _events_arg(pb: PreparedBatch, events):
+        if events is None:
+            return None
+        return (ctypes.c_void_p * (2 * pb.n_launches))(*[int(e) if e else None for e in events])
+
+    def run(self, pb: PreparedBatch, events=None, stream=None):
+        """Stats + fused launch(es) of one batch on one stream (``slg_reconstruct_batch``).
+        ``events``: 2 raw hipEvent_t per fused launch (timing), or None."""
+        N.check(N.lib().slg_reconstruct_batch(pb.caps, pb.n, ctypes.byref(pb.dp), ctypes.byref(pb.calib),
+                                              ctypes.byref(pb.tp), self._ws(pb.slot), self.ws_stride,
+                                              pb.clouds, self._events_arg(pb, events), _stream(stream)))
+
+    def stats(self, pb: PreparedBatch, stream=None):
+        N.check(N.lib().slg_decode_stats_batch(pb.caps, pb.n, ctypes.byref(pb.dp), self._ws(pb.slot),
+                                               self.ws_stride, _stream(stream)))
+
+    def main(self, pb: PreparedBatch, events=None, stream=None):
+        N.check(N.lib().slg_decode_triangulate_batch(pb.caps, pb.n, ctypes.byref(pb.dp),
+                                                     ctypes.byref(pb.calib), ctypes.byref(pb.tp),
+                                                     self._ws(pb.slot), self.ws_stride, pb.clouds,
+                                                     self._events_arg(pb, events), _stream(stream)))
+
+    def run_pipelined(self, batches, main_stream, stats_stream, events=None):
+        """Run ``batches`` (PreparedBatch list; consecutive ones on different slots) with the
+        stats of batch k+1 on ``stats_stream`` overlapping batch k's fused launch on
+        ``main_stream``.  ``events[k]``: timing events for batch k's fused launches, or None."""
+        n = len(batches)
+        for k in range(1, n):
+            if batches[k].slot == batches[k - 1].slot:
+                raise ValueError("consecutive batches must use different workspace slots")
+        while len(self._events) < 2 * n:
+            self._events.append(torch.cuda.Event())
+        st_ev, mn_ev = self._events[0::2], self._events[1::2]
+        if n:
+            self.stats(batches[0], stream=stats_stream)
+            st_ev[0].record(stats_stream)
+        for k in range(n):
+            if k + 1 < n:
+                if k >= 1:                                 # batch k+1 reuses batch k-1's slot
+                    stats_stream.wait_event(mn_ev[k - 1])
+                self.stats(batches[k + 1], stream=stats_stream)
+                st_ev[k + 1].record(stats_stream)
+            main_stream.wait_event(st_ev[k])
+            self.main(batches[k], events=None if events is None else events[k], stream=main_stream)
+            mn_ev[k].record(main_stream)
+        if n:
+            stats_stream.wait_event(mn_ev[n - 1])          # callers may sync either stream

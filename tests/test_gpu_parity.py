@@ -317,3 +317,36 @@ def test_batch_api_matches_single_view(mods):
                 P, C = o.result()
                 assert np.array_equal(P.cpu().numpy(), seq[k]["P1"]), names[k % len(names)]
                 assert np.array_equal(C.cpu().numpy(), seq[k]["C1"])
+
+
+def test_batch_pipelined_matches_golden(mods):
+    """BatchReconstructor.run_pipelined: stats of batch k+1 on a side stream while batch k's
+    fused launch runs (alternating workspace slots); ragged batches, views with different
+    frame counts in one launch, and a batch spanning two launches (> 16 views)."""
+    E, PR, N = mods
+    import torch
+    names = ["proc_otsu_full", "proc_c2style", "proc_missing_odd", "proc_flat_ties", "proc_manual_float"]
+    cal = load_calibs()["rig"]
+    zs = [load_case(n) for n in names]
+    H, W = zs[0]["mask"].shape
+    dc = E.DeviceCalib(cal, H, W)
+    cfg = E.DecodeConfig(1920, 1080, 11, 11, "otsu")
+    seq = [z for z in zs * 6 if z["params"].get("thresh_mode", "otsu") == "otsu"
+           and z["params"].get("n_sets_col", 11) == 11 and z["params"].get("n_sets_row", 11) == 11]
+    assert len({z["frames"].shape[0] for z in seq}) > 1        # mixed frame counts per launch
+    frames = [E.DeviceFrames(list(z["frames"]), z["texture"]) for z in seq]
+    assert len(seq) == 18
+    for sizes in ([7, 7, 4], [18]):
+        eng = E.BatchReconstructor(H, W, max(sizes), slots=2)
+        outs, batches, j = [], [], 0
+        for n in sizes:
+            o = [E.Cloud(H * W, 1, True) for _ in range(n)]
+            batches.append(eng.prepare(frames[j:j + n], cfg, dc, o, row_mode=1, slot=len(batches) % 2))
+            outs += o
+            j += n
+        s_main, s_stats = torch.cuda.Stream(), torch.cuda.Stream()
+        eng.run_pipelined(batches, s_main, s_stats)
+        torch.cuda.synchronize()
+        for z, o in zip(seq[:j], outs):
+            P, C = o.result()
+            assert np.array_equal(P.cpu().numpy(), z["P1"]) and np.array_equal(C.cpu().numpy(), z["C1"])

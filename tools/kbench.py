@@ -25,7 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--size", default="1920x1080")
-    ap.add_argument("--views", type=int, default=6)
+    ap.add_argument("--views", type=int, default=12)
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     import numpy as np
@@ -82,16 +82,52 @@ def main():
         pts[rm] = int(clouds[rm].count.item())
         frame_b = (2 + 2 * 11 + (2 * 10 if rm else 0)) * n_px
         run(f"main_rm{rm}", f, pre=lambda v: eng.stats(dfr[v], cfg), alg_bytes=frame_b + 18 * pts[rm])
+    # batched fused launches: all pool views in ONE main3 launch (stats done beforehand)
+    frame_b1 = (2 + 2 * 11 + 2 * 10) * n_px
+    for nb in sorted({min(6, len(dfr)), len(dfr)}):
+        beng = E.BatchReconstructor(H, W, nb)
+        bclouds = [E.Cloud(H * W, 1, False) for _ in range(nb)]
+        pb = beng.prepare(dfr[:nb], cfg, dcal, bclouds, 1)
+        beng.stats(pb)
+        torch.cuda.synchronize()
+        run(f"stats_batch{nb}", lambda v: beng.stats(pb))
+        tags = [("", None)]
+        if nb == len(dfr):
+            tags += [(f"_dbg{d}", str(d)) for d in (1, 2, 4, 7)]
+            tags += [(f"_nap{c}", str(c << 8)) for c in (1, 2, 4, 16, 64)]
+        for tag, dbg in tags:
+            if dbg:
+                os.environ["SLG_DBG"] = dbg
+            name = f"main3_batch{nb}{tag}"
+            run(name, lambda v: beng.main(pb), pre=lambda v: beng.stats(pb),   # stats re-arm the look-back
+                alg_bytes=nb * (frame_b1 + 18 * pts[1]))
+            os.environ.pop("SLG_DBG", None)
+            if name in res:
+                res[name]["per_view_us"] = round(res[name]["median_us"] / nb, 2)
+                print(name, "per view", res[name]["per_view_us"], file=sys.stderr, flush=True)
+    # pipelined: stats of batch k+1 on a side stream during batch k's fused launch
+    nb = len(dfr)
+    beng = E.BatchReconstructor(H, W, nb, slots=2)
+    bclouds = [[E.Cloud(H * W, 1, False) for _ in range(nb)] for _ in range(2)]
+    pbs = [beng.prepare(dfr, cfg, dcal, bclouds[k], 1, slot=k) for k in range(2)]
+    s2 = torch.cuda.Stream()
+    for rep in range(2):
+        seq = [pbs[k % 2] for k in range(8)]
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record(s)
+        s2.wait_stream(s)
+        beng.run_pipelined(seq, s, s2)
+        s.wait_stream(s2)
+        b.record(s)
+        torch.cuda.synchronize()
+        us = a.elapsed_time(b) * 1e3 / (8 * nb)
+    res["pipelined_per_view_us"] = round(us, 2)
+    print("pipelined per view", round(us, 2), file=sys.stderr, flush=True)
     run("decode", lambda v: eng.decode(dfr[v], cfg), alg_bytes=(44 + 9) * n_px)
     run("tri_rm1", lambda v: eng.triangulate(maps[v][0], maps[v][1], maps[v][2], dfr[v].texture, dcal, 1,
                                              xyz_f64=False, out=clouds[1]),
         alg_bytes=9 * n_px + 18 * pts[1])
-    os.environ["SLG_MAIN"] = "1"
-    run("main_rm1_gen1", lambda v: eng.decode_triangulate(dfr[v], cfg, dcal, clouds[1], 1),
-        pre=lambda v: eng.stats(dfr[v], cfg))
-    run("tri_rm1_gen1", lambda v: eng.triangulate(maps[v][0], maps[v][1], maps[v][2], dfr[v].texture,
-                                                 dcal, 1, xyz_f64=False, out=clouds[1]))
-    os.environ.pop("SLG_MAIN")
     os.environ["SLG_DBG"] = "16"
     run("stats_no_otsu", lambda v: eng.stats(dfr[v], cfg))
     for dbg in (8, 15, 1, 2, 4, 3, 7):
