@@ -7,9 +7,10 @@ filter, tol 2.0), fp32 XYZ + BGR out.  Every step does the full path for its vie
 resident in HBM: the stats pass (histograms -> Otsu thresholds) and the fused
 decode/triangulate/compaction pass.  Steps rotate over a pool of distinct rendered turntable
 views (12 x 95 MB frame stacks > 256 MiB Infinity Cache) so frames stream from HBM.  Views are
-issued in batches (C3/C5 style): one fused main3 launch per batch of up to 16 views, with the
-batched stats launch of batch k+1 on a side stream overlapping batch k's fused launch
-(BatchReconstructor.run_pipelined).  One process per GPU (torchrun); each rank renders its own
+issued in batches (C3/C5 style): per batch of up to 16 views one batched stats launch and one
+fused main3 launch; the next batch's stats run on a side stream during this batch's fused
+launch (BatchReconstructor.run_pipelined; --pipeline serial: both on one stream,
+slg_reconstruct_batch).  One process per GPU (torchrun); each rank renders its own
 views (weak scaling, no data-path collective); value = all ranks' points / max-over-ranks time.
 
 Prints ONE JSON line on stdout (rank 0).  Diagnostics go to stderr.
@@ -72,6 +73,9 @@ def main():
     ap.add_argument("--views", type=int, default=12, help="distinct rendered views in the pool")
     ap.add_argument("--batch", type=int, default=12, help="views per fused launch (<= 16)")
     ap.add_argument("--xyz", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--pipeline", choices=["serial", "overlap"], default="overlap",
+                    help="serial: stats + fused launch per batch on one stream; overlap: the next "
+                         "batch's stats on a side stream during this batch's fused launch")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -148,14 +152,21 @@ def main():
         total_pts += pts[v % len(views)]
         bytes_alg += frame_b + out_b * pts[v % len(views)]
 
+    def run_all(batches, events=None):
+        if args.pipeline == "overlap":
+            beng.run_pipelined(batches, s_main, s_stats, events=events)
+        else:
+            for k, pb in enumerate(batches):
+                beng.run(pb, events=None if events is None else events[k], stream=s_main)
+
     if warm:
-        beng.run_pipelined(warm, s_main, s_stats)
+        run_all(warm)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    beng.run_pipelined(timed, s_main, s_stats, events=[(a.cuda_event, b.cuda_event) for a, b in ev])
+    run_all(timed, events=[(a.cuda_event, b.cuda_event) for a, b in ev])
     t_enq = time.perf_counter() - t0              # host time to enqueue the K steps
     torch.cuda.synchronize()
     if world > 1:
@@ -210,6 +221,7 @@ def main():
                        "views_per_rank": len(views), "points_per_view": int(np.mean(pts)),
                        "batch_views": B,
                        "launches": n_launch,
+                       "stats_pipeline": args.pipeline,
                        "lookback_helper_runs": helper_runs,
                        "host_enqueue_ms_per_step": round(t_enq / K * 1e3, 4),
                        "decode": "u8 compares, int32 codes; triangulation f64",

@@ -115,6 +115,7 @@ __device__ inline uint32_t gray2bin_x2(uint32_t x) {
 // ------------------------------------------------------------------ stats kernel
 constexpr int kMaxBatch = 16;               // views per batched stats launch (blockIdx.y)
 constexpr int kStatsPx = 32;                // pixels per lane per stats iteration
+constexpr int kStatsBlocks = 64;            // stats workgroups per view (at most)
 
 struct StatsParams {
   const uint8_t* white[kMaxBatch];
@@ -128,6 +129,21 @@ struct StatsParams {
   double contrast_val;
   int32_t dbg;             // profiling ablation (SLG_DBG bit 4: skip the Otsu tail)
 };
+
+// a / b correctly rounded from y = RN(1/b) (Markstein): with y correctly rounded and q1
+// faithful, q2 = RN(q1 + (a - b*q1) * y) = RN(a / b); q0 = RN(a*y) is within 1.5 ulp, so one
+// correction makes q1 faithful and the second one is exact (tools/markstein_check.c checks it
+// against IEEE division).  Valid while nothing over/underflows: div_rn_ok() vets a, the
+// caller vets b and y.
+__device__ inline double div_rn(double a, double b, double y) {
+  const double q0 = a * y;
+  const double q1 = fma(fma(-b, q0, a), y, q0);
+  return fma(fma(-b, q1, a), y, q1);
+}
+__device__ inline bool div_rn_ok(double a) {
+  const double m = fabs(a);
+  return m == 0.0 || (m > 0x1p-900 && m < 0x1p900);
+}
 
 // OpenCV getThreshVal_Otsu_8u (see oracle/sl_oracle.py:otsu_from_hist) evaluated by one wave.
 // Bit-exact with the sequential fp64 loop: only order-independent pieces run in parallel.
@@ -236,7 +252,10 @@ __device__ float percentile95_from_hist(const uint32_t* h, int64_t n) {
 }
 
 __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
-  __shared__ uint32_t sh[4][2][256];        // per-wave sub-histograms (less LDS atomic contention)
+  // 16 sub-histograms per kind (wave x lane&3), rows padded to 257 words so the copies of one
+  // bin sit in different banks: a flat background costs at most 16-way same-address adds.
+  constexpr int kRow = 257;
+  __shared__ uint32_t sh[16 * 2 * kRow];
   __shared__ uint32_t s_maxd;
   __shared__ uint32_t s_last;
   const int tid = threadIdx.x;
@@ -262,57 +281,49 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
     return;
   }
 
-  for (int i = tid; i < 4 * 2 * 256; i += kBlock) (&sh[0][0][0])[i] = 0;
+  for (int i = tid; i < 16 * 2 * kRow; i += kBlock) sh[i] = 0;
   if (tid == 0) s_maxd = 0;
   __syncthreads();
 
-  // hist slots: otsu -> [0] white, [1] clip(white-black); percentile -> [0] black.
-  // Each lane takes kStatsPx consecutive pixels (all loads issued before any is consumed).
+  // hist kinds: otsu -> [0] white, [1] clip(white-black); percentile -> [0] black.
+  // Each lane takes kStatsPx consecutive pixels per step (all loads issued before use).
   const bool otsu = p.thresh_mode == SLG_THRESH_OTSU;
+  uint32_t* h0 = sh + (4 * wave + (tid & 3)) * 2 * kRow;
+  uint32_t* h1 = h0 + kRow;
   uint32_t local_max = 0;
   const int64_t per_block = int64_t(kBlock) * kStatsPx;
   for (int64_t b0 = int64_t(blockIdx.x) * per_block; b0 < p.n_px; b0 += int64_t(gridDim.x) * per_block) {
-    const int64_t px0 = b0 + int64_t(tid) * kStatsPx;  // whole waves iterate together (ballots below)
-    const int64_t lp = px0 < p.n_px ? px0 : 0;           // frames are readable up to round_up(n, 8)
+    const int64_t px0 = b0 + int64_t(tid) * kStatsPx;
     uint2 w[kStatsPx / 8], b[kStatsPx / 8];
 #pragma unroll
     for (int q = 0; q < kStatsPx / 8; ++q) {
-      const int64_t o = lp + 8 * q < p.n_px ? lp + 8 * q : 0;
+      const int64_t o = px0 + 8 * q < p.n_px ? px0 + 8 * q : 0;   // frames readable to round_up(n, 8)
       w[q] = *reinterpret_cast<const uint2*>(white + o);
       b[q] = *reinterpret_cast<const uint2*>(black + o);
     }
 #pragma unroll
     for (int k = 0; k < kStatsPx; ++k) {
-      const bool ok = px0 + k < p.n_px;
+      if (px0 + k >= p.n_px) break;
       const uint2 wq = w[k >> 3], bq = b[k >> 3];
       const int wv = (((k & 7) < 4 ? wq.x : wq.y) >> (8 * (k & 3))) & 0xff;
       const int bv = (((k & 7) < 4 ? bq.x : bq.y) >> (8 * (k & 3))) & 0xff;
       const int d = wv - bv;
-      // Skewed images put many lanes of a wave on one bin (dark background: clip(w-b) = 0);
-      // lanes equal to the first active lane's value are counted with one ballot + one add.
-      const int v0 = otsu ? wv : bv;
-      const int v1 = d < 0 ? 0 : d;
-      const uint64_t act = __ballot(ok);
-      if (act) {
-        const int lead = __ffsll((unsigned long long)act) - 1;
-        const int l0 = __shfl(v0, lead);
-        const uint64_t m0 = __ballot(ok && v0 == l0);
-        if ((threadIdx.x & 63) == lead) atomicAdd(&sh[wave][0][l0], uint32_t(__popcll(m0)));
-        else if (ok && v0 != l0) atomicAdd(&sh[wave][0][v0], 1u);
-        if (otsu) {
-          const int l1 = __shfl(v1, lead);
-          const uint64_t m1 = __ballot(ok && v1 == l1);
-          if ((threadIdx.x & 63) == lead) atomicAdd(&sh[wave][1][l1], uint32_t(__popcll(m1)));
-          else if (ok && v1 != l1) atomicAdd(&sh[wave][1][v1], 1u);
-        }
+      if (otsu) {
+        atomicAdd(&h0[wv], 1u);
+        atomicAdd(&h1[d < 0 ? 0 : d], 1u);
+      } else {
+        atomicAdd(&h0[bv], 1u);
+        local_max = max(local_max, uint32_t(d + 256));
       }
-      if (!otsu && ok) local_max = max(local_max, uint32_t(d + 256));
     }
   }
   if (!otsu) atomicMax(&s_maxd, local_max);
   __syncthreads();
   for (int i = tid; i < 2 * 256; i += kBlock) {
-    const uint32_t v = (&sh[0][0][0])[i] + (&sh[1][0][0])[i] + (&sh[2][0][0])[i] + (&sh[3][0][0])[i];
+    const int kind = i >> 8, bin = i & 255;
+    uint32_t v = 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v += sh[(2 * c + kind) * kRow + bin];
     if (v) atomicAdd(hist_part + (blockIdx.x % kHistCopies) * 512 + i, v);
   }
   if (!otsu && tid == 0 && s_maxd) atomicMax(&ws->max_diff_enc, s_maxd);
@@ -335,7 +346,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  uint32_t* hg = &sh[0][0][0];                 // reuse wave-0 slots for the global histograms
+  uint32_t* hg = sh;                           // reuse the sub-histograms for the global ones
   for (int i = tid; i < 2 * 256; i += kBlock)
   {
     uint32_t acc = 0;
@@ -393,6 +404,9 @@ struct MainParams {
   // calibration
   const double* rays;
   double fx, fy, cx, cy;
+  double rfx, rfy;            // RN(1/fx), RN(1/fy) when div_fast (Markstein divisions)
+  int32_t div_fast;
+  int32_t pad1;
   double o0, o1, o2;
   const double* pcol;
   int32_t n_pcol;
@@ -544,10 +558,18 @@ __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int
   }
   double r0, r1, r2;
   if (RAYS == SLG_RAYS_PINHOLE) {
-    const double x = (double(u) - p.cx) / p.fx;            // processing.py:150
-    const double y = (double(v) - p.cy) / p.fy;            // processing.py:151
+    // The same IEEE quotients as the reference, with the divisions by fx, fy (per camera)
+    // and by the norm (three per pixel) done as Markstein corrections of one reciprocal.
+    const double ax = double(u) - p.cx, ay = double(v) - p.cy;
+    const double x = p.div_fast && div_rn_ok(ax) ? div_rn(ax, p.fx, p.rfx) : ax / p.fx;   // processing.py:150
+    const double y = p.div_fast && div_rn_ok(ay) ? div_rn(ay, p.fy, p.rfy) : ay / p.fy;   // processing.py:151
     const double n = sqrt((x * x + y * y) + 1.0);          // np.linalg.norm(rays, axis=0)
-    r0 = x / n; r1 = y / n; r2 = 1.0 / n;                  // rays /= norms
+    r2 = 1.0 / n;                                          // rays /= norms
+    if (n < 0x1p900 && div_rn_ok(x) && div_rn_ok(y)) {     // n >= 1: its reciprocal is normal
+      r0 = div_rn(x, n, r2); r1 = div_rn(y, n, r2);
+    } else {
+      r0 = x / n; r1 = y / n;
+    }
   } else {
     const int64_t px = int64_t(v) * p.width + u;
     r0 = p.rays[px]; r1 = p.rays[p.n_px + px]; r2 = p.rays[2 * p.n_px + px];
@@ -1090,8 +1112,10 @@ int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* black
   sp.shadow_val = dp ? dp->shadow_val : 0.0;
   sp.contrast_val = dp ? dp->contrast_val : 0.0;
   sp.dbg = debug_flags();
+  // Few fat workgroups per view: each merges its sub-histograms into the view's histogram with
+  // <= 512 global atomics, and a batch's stats pass takes few CU slots next to a fused launch.
   int64_t grid = (n_px + int64_t(kBlock) * kStatsPx - 1) / (int64_t(kBlock) * kStatsPx);
-  if (grid > 1024) grid = 1024;
+  if (grid > kStatsBlocks) grid = kStatsBlocks;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(stats_kernel, dim3(unsigned(grid), unsigned(n_views)), dim3(kBlock), 0, s, sp);
   return check_launch("stats_kernel");
@@ -1113,6 +1137,13 @@ int fill_calib(MainParams& mp, const slg_calib* c, const slg_tri_params* tp, int
     return fail(SLG_ERR_INVALID, "plane tables must be 16-byte aligned");
   mp.rays = c->rays;
   mp.fx = c->fx; mp.fy = c->fy; mp.cx = c->cx; mp.cy = c->cy;
+  auto vetted = [](double b) {                     // b and RN(1/b) normal, far from over/underflow
+    const double m = fabs(b);
+    return std::isfinite(b) && m > 0x1p-900 && m < 0x1p900;
+  };
+  mp.rfx = 1.0 / c->fx;
+  mp.rfy = 1.0 / c->fy;
+  mp.div_fast = vetted(c->fx) && vetted(c->fy) ? 1 : 0;
   mp.o0 = c->oc[0]; mp.o1 = c->oc[1]; mp.o2 = c->oc[2];
   mp.pcol = c->col_planes; mp.n_pcol = c->n_col_planes;
   mp.prow = c->row_planes; mp.n_prow = c->n_row_planes;

@@ -124,6 +124,17 @@ def main():
         us = a.elapsed_time(b) * 1e3 / (8 * nb)
     res["pipelined_per_view_us"] = round(us, 2)
     print("pipelined per view", round(us, 2), file=sys.stderr, flush=True)
+    for rep in range(2):                             # stats + fused launch on one stream
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record(s)
+        for k in range(8):
+            beng.run(pbs[k % 2], stream=s)
+        b.record(s)
+        torch.cuda.synchronize()
+        us = a.elapsed_time(b) * 1e3 / (8 * nb)
+    res["serial_per_view_us"] = round(us, 2)
+    print("serial per view", round(us, 2), file=sys.stderr, flush=True)
     run("decode", lambda v: eng.decode(dfr[v], cfg), alg_bytes=(44 + 9) * n_px)
     run("tri_rm1", lambda v: eng.triangulate(maps[v][0], maps[v][1], maps[v][2], dfr[v].texture, dcal, 1,
                                              xyz_f64=False, out=clouds[1]),
