@@ -42,7 +42,12 @@ namespace {
 
 constexpr int kBlock = 256;                 // 4 waves of 64
 constexpr int kPx = 8;                      // pixels per lane (one 8-byte load per frame)
-constexpr int kTilePx = kBlock * kPx;       // 2048 pixels per workgroup tile
+#ifndef SLG_TILE_BLOCK
+#define SLG_TILE_BLOCK 256
+#endif
+constexpr int kTileBlock = SLG_TILE_BLOCK;  // main3 workgroup (512 measured slower: 31.3 vs 30.2 us/view)
+constexpr int kTilePx = kTileBlock * kPx;   // 2048 pixels per main3 tile (one look-back entry)
+constexpr int kMapsPx = kBlock * kPx;       // 2048 pixels per decode_maps workgroup
 constexpr int kMaxBits = 15;                // packed 16-bit code lanes
 constexpr int kLookK = 2;                  // look-back window = 2 x 64 predecessor tiles per poll
 constexpr uint64_t kFlagAgg = 1ull << 62;
@@ -719,10 +724,10 @@ __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int ag
   return true;
 }
 
-// Correspondence maps of one 2048-pixel tile (slg_decode): col/row int32, mask uint8.
+// Correspondence maps of 2048 pixels per workgroup (slg_decode): col/row int32, mask uint8.
 __global__ __launch_bounds__(kBlock) void decode_maps_kernel(MainParams p) {
-  const int64_t px0 = int64_t(blockIdx.x) * kTilePx + int64_t(threadIdx.x) * kPx;
-  const bool tail = int64_t(blockIdx.x) == p.n_tiles - 1;
+  const int64_t px0 = int64_t(blockIdx.x) * kMapsPx + int64_t(threadIdx.x) * kPx;
+  const bool tail = px0 + kPx > p.n_px;       // lane-level guard for the ragged end
   uint32_t valid;
   int col[kPx], row[kPx];
   decode_lane<1, 1, 8>(p, px0, tail, valid, col, row);
@@ -755,8 +760,8 @@ __global__ __launch_bounds__(kBlock) void decode_maps_kernel(MainParams p) {
 // Per 256-lane workgroup and 2048-pixel tile:
 //  A  every lane decodes its 8 pixels (all used frames in flight, 8-byte coalesced loads); a
 //     block scan compacts the tile's valid pixels into LDS items (code, BGR, pixel offset);
-//  B  the 256 lanes triangulate the items 256 at a time (fp64, NumPy order) -- balanced over
-//     the four waves whatever the foreground layout; points stay in registers and one ballot
+//  B  the lanes triangulate the items one workgroup-width at a time (fp64, NumPy order) --
+//     balanced over the waves whatever the foreground layout; points stay in registers and one ballot
 //     per wave and round gives every kept point its rank;
 //  C  one barrier shares the per-(round, wave) counts, wave 0 resolves the tile's offset by
 //     decoupled look-back (helping a long-silent predecessor, so waiting always ends);
@@ -828,7 +833,7 @@ __device__ inline int2 block_scan(int x, int* s_wtot) {
   __syncthreads();
   int off = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < kBlock / 64; ++w) {
+  for (int w = 0; w < kTileBlock / 64; ++w) {
     off += w < wave ? s_wtot[w] : 0;
     tot += s_wtot[w];
   }
@@ -836,15 +841,16 @@ __device__ inline int2 block_scan(int x, int* s_wtot) {
 }
 
 template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS>
-__global__ __launch_bounds__(kBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) void main3_kernel(Main3Params P) {
+__global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) void main3_kernel(Main3Params P) {
   using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
   constexpr int NS = ROW_MODE == 2 ? 2 : 1;
-  constexpr int kIt = kTilePx / kBlock;    // 8 item rounds of 256 at most
+  constexpr int kB = kTileBlock;
+  constexpr int kIt = kTilePx / kB;        // 8 item rounds of one workgroup at most
   __shared__ uint32_t s_code[kTilePx];     // valid item: col | row << 16
   __shared__ uint32_t s_bgr[kTilePx];      // its BGR (24 bits)
   __shared__ uint16_t s_off[kTilePx];      // its pixel offset inside the tile
-  __shared__ int s_wtot[kBlock / 64];
-  __shared__ int s_cnt[NS][kIt][kBlock / 64];   // kept points per (round, wave)
+  __shared__ int s_wtot[kB / 64];
+  __shared__ int s_cnt[NS][kIt][kB / 64];  // kept points per (round, wave)
   __shared__ uint64_t s_excl[NS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -886,17 +892,19 @@ __global__ __launch_bounds__(kBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) 
   __syncthreads();
 
   // ------------------------------------------------------------ B: triangulate, balanced
-  // Item m = tid + 256 * i: every wave gets a quarter of the tile's valid pixels.
+  // Item m = tid + kB * i: every wave gets an equal share of the tile's valid pixels.
   const int v0 = int(tile_px / p.width);
   const int u0 = int(tile_px - int64_t(v0) * p.width);
+  // Points stay in registers across the look-back (recomputing them after it instead frees
+  // ~15 VGPRs for a fifth wave per SIMD but measured 6% slower).
   XT pts[NS][kIt][3];
   uint64_t km[NS][kIt];
 #pragma unroll
   for (int i = 0; i < kIt; ++i) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) km[s][i] = 0;
-    if (i * kBlock < n_items) {                      // block-uniform
-      const int m = tid + kBlock * i;
+    if (i * kB < n_items) {                          // block-uniform
+      const int m = tid + kB * i;
       const bool in = m < n_items;
       const uint32_t code = in ? s_code[m] : 0u;
       int u = u0 + (in ? int(s_off[m]) : 0), v = v0;
@@ -927,7 +935,7 @@ __global__ __launch_bounds__(kBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) 
 #pragma unroll 1
     for (int s = 0; s < NS; ++s) {
       int agg = 0;
-      for (int q = 0; q < kIt * (kBlock / 64); ++q) agg += (&s_cnt[s][0][0])[q];
+      for (int q = 0; q < kIt * (kB / 64); ++q) agg += (&s_cnt[s][0][0])[q];
       uint64_t* st = p.states + int64_t(s) * tiles;
       uint64_t excl;
       int ht;
@@ -963,7 +971,7 @@ __global__ __launch_bounds__(kBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) 
     for (int i = 0; i < kIt; ++i) {
       int before = 0, round = 0;
 #pragma unroll
-      for (int w = 0; w < kBlock / 64; ++w) {
+      for (int w = 0; w < kB / 64; ++w) {
         const int c = s_cnt[s][i][w];
         before += w < wave ? c : 0;
         round += c;
@@ -971,7 +979,7 @@ __global__ __launch_bounds__(kBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) 
       if ((km[s][i] >> lane) & 1ull) {
         const int64_t q = base + before + __popcll(km[s][i] & lt);
         gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
-        const uint32_t c = s_bgr[tid + kBlock * i];
+        const uint32_t c = s_bgr[tid + kB * i];
         gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
       }
       base += round;
@@ -1201,7 +1209,7 @@ int launch_main3(Main3Fn fn, Main3Params& mp, const slg_tri_params* tp, const sl
   mp.c.dbg = debug_flags();
   const int64_t grid = mp.c.n_tiles * mp.n_views;
   if (grid > INT_MAX) return fail(SLG_ERR_UNSUPPORTED, "batch too large for one launch");
-  hipLaunchKernelGGL(fn, dim3(unsigned(grid)), dim3(kBlock), 0, s, mp);
+  hipLaunchKernelGGL(fn, dim3(unsigned(grid)), dim3(kTileBlock), 0, s, mp);
   int rc = check_launch("main kernel");
   if (rc || !tp || tp->row_mode != 2) return rc;
   const unsigned tg = unsigned((mp.c.n_px + kBlock - 1) / kBlock);
@@ -1408,7 +1416,7 @@ int32_t slg_decode(const slg_capture* cap, const slg_decode_params* dp, void* wo
   mp.out_col = col_out; mp.out_row = row_out; mp.out_mask = mask_out;
   mp.ws = reinterpret_cast<WsHeader*>(workspace);
   mp.n_tiles = n_tiles_of(n_px);
-  hipLaunchKernelGGL(decode_maps_kernel, dim3(unsigned(mp.n_tiles)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(decode_maps_kernel, dim3(unsigned((n_px + kMapsPx - 1) / kMapsPx)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), mp);
   return check_launch("decode_maps_kernel");
 }
