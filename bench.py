@@ -53,14 +53,15 @@ def cpu_baseline(views, cal, seconds):
                       f"memory, oracle/sl_oracle.py NumPy restatement, 1 thread, {dt:.1f} s"}
 
 
-def load_traffic():
-    """HBM bytes per main_kernel launch from the committed rocprofv3 PMC summary, if any."""
+def load_traffic_per_view():
+    """HBM bytes per view of the fused kernel from the committed rocprofv3 PMC summary
+    (profiles/pmc_main_kernel.json, written by tools/summarize_profile.py), if any."""
     p = os.path.join(ROOT, "profiles", "pmc_main_kernel.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            return json.load(f).get("hbm_bytes_per_view")
     except (OSError, ValueError):
         return None
 
@@ -69,7 +70,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=24)
     ap.add_argument("--views", type=int, default=12, help="distinct rendered views in the pool")
     ap.add_argument("--batch", type=int, default=12, help="views per fused launch (<= 16)")
     ap.add_argument("--xyz", choices=["f32", "f64"], default="f32")
@@ -121,12 +122,13 @@ def main():
             preps[key] = beng.prepare(fr, cfg, dcal, clouds[slot][:n], row_mode, tol, slot=slot)
         return preps[key]
 
-    # points per view (and a sanity pass over the pool)
+    # points per view: one sanity pass over the pool in batches of B (same launch shape as timed)
     pts = []
-    for v in range(len(views)):
-        beng.run(prep(v, 1, 0), stream=s_main)
+    for v0 in range(0, len(views), B):
+        n = min(B, len(views) - v0)
+        beng.run(prep(v0, n, 0), stream=s_main)
         s_main.synchronize()
-        pts.append(int(clouds[0][0].count.item()))
+        pts += [int(clouds[0][k].count.item()) for k in range(n)]
 
     def batches_for(first, count):
         """Steps [first, first+count) as batches of <= B views on alternating slots."""
@@ -194,7 +196,8 @@ def main():
         kern_avg_s = kern_sum / launches / 1e3
         achieved = bytes_sum / launches / kern_avg_s / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(),
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": (round(load_traffic_per_view() * K / n_launch) if load_traffic_per_view() else None),
                 "kernel": "main3_kernel<1,0,1,1> (fused decode+triangulate+compaction, "
                           f"{B} views per launch)",
                 "kernel_avg_us": round(kern_avg_s * 1e6, 2),

@@ -1,12 +1,16 @@
 #!/usr/bin/env python
 """Copy a gpu_profile.sh run (gpurun_out/<tag>) into profiles/<tag>/ and summarise it.
 
-  python tools/summarize_profile.py r1a [--kernel main2_kernel]
+  python tools/summarize_profile.py r1b [--kernel main3_kernel] [--tiles-per-view 1013]
 
-Writes profiles/<tag>/{bench.json, kernel_stats.csv, pmc_summary.json} and refreshes
-profiles/pmc_main_kernel.json (HBM bytes per launch of the dominant kernel, read by bench.py as
-`roofline.traffic`).  HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are
-in KiB; on gfx950 FETCH_SIZE counts half the bytes of wide streaming reads, so it is doubled.
+Writes profiles/<tag>/{bench.json, kernel_stats.csv, kernel_by_grid.json, pmc_summary.json} and
+refreshes profiles/pmc_main_kernel.json, which bench.py reads for `roofline.traffic`.
+
+The fused kernel runs one launch per batch of views, so launches of different sizes appear in
+one trace (the bench's sanity pass, a ragged last batch).  Durations and bytes are therefore
+grouped by grid size, and the HBM bytes are normalised per VIEW (grid threads / 256 lanes /
+tiles per view).  HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in
+KiB; on gfx950 FETCH_SIZE counts half the bytes of wide streaming reads, so it is doubled.
 """
 from __future__ import annotations
 
@@ -19,21 +23,21 @@ import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LANES = 256
 
 
-def per_kernel(path, counter):
-    d = collections.defaultdict(list)
+def rows_of(path, kernel):
+    if not os.path.exists(path):
+        return []
     with open(path) as f:
-        for r in csv.DictReader(f):
-            if r["Counter_Name"] == counter:
-                d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return d
+        return [r for r in csv.DictReader(f) if kernel in r["Kernel_Name"]]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--kernel", default="main2_kernel")
+    ap.add_argument("--kernel", default="main3_kernel")
+    ap.add_argument("--tiles-per-view", type=int, default=1013, help="ceil(1920*1080 / 2048)")
     a = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", a.tag)
     dst = os.path.join(ROOT, "profiles", a.tag)
@@ -42,33 +46,41 @@ def main():
                  ("bench_trace.json", "bench_trace.json")):
         if os.path.exists(os.path.join(src, s)):
             shutil.copy(os.path.join(src, s), os.path.join(dst, d))
+    grid_threads_per_view = LANES * a.tiles_per_view
+
+    # kernel trace: duration per launch grouped by grid size
+    by_grid = collections.defaultdict(list)
+    for r in rows_of(os.path.join(src, "trace", "trace_kernel_trace.csv"), a.kernel):
+        by_grid[int(r["Grid_Size_X"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    trace = {str(g): {"views": g / grid_threads_per_view, "launches": len(d),
+                      "avg_us": round(statistics.mean(d), 2),
+                      "avg_us_per_view": round(statistics.mean(d) / (g / grid_threads_per_view), 2)}
+             for g, d in sorted(by_grid.items())}
+    with open(os.path.join(dst, "kernel_by_grid.json"), "w") as f:
+        json.dump({"kernel": a.kernel, "by_grid_threads": trace}, f, indent=1)
+
+    # PMC: HBM bytes per view
     out = {"source": f"gpurun_out/{a.tag}", "kernel": a.kernel,
-           "units": "bytes per launch; FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read correction), "
-                    "WRITE_SIZE KiB x 1024"}
-    fetch = per_kernel(os.path.join(src, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(src, "write", "write_counter_collection.csv"), "WRITE_SIZE")
-    kern = {}
-    for name in sorted(set(fetch) | set(write)):
-        f = fetch.get(name, [])
-        w = write.get(name, [])
-        kern[name] = {"launches": max(len(f), len(w)),
-                      "fetch_bytes": round(statistics.mean(f) * 1024 * 2) if f else None,
-                      "write_bytes": round(statistics.mean(w) * 1024) if w else None}
-    out["kernels"] = kern
-    main_k = [n for n in kern if a.kernel in n]
-    if main_k:
-        k = kern[main_k[0]]
-        out["hbm_bytes_per_launch"] = (k["fetch_bytes"] or 0) + (k["write_bytes"] or 0)
-        out["main_kernel_name"] = main_k[0]
+           "units": "bytes; FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read correction), WRITE_SIZE KiB x 1024"}
+    per = {}
+    for pmc, key, scale in (("fetch", "FETCH_SIZE", 2048), ("write", "WRITE_SIZE", 1024)):
+        rows = rows_of(os.path.join(src, pmc, f"{pmc}_counter_collection.csv"), a.kernel)
+        rows = [r for r in rows if r["Counter_Name"] == key]
+        if rows:
+            views = sum(int(r["Grid_Size"]) / grid_threads_per_view for r in rows)
+            per[key] = sum(float(r["Counter_Value"]) * scale for r in rows) / views
+            out[key.lower() + "_bytes_per_view"] = round(per[key])
+            out[key.lower() + "_launches"] = len(rows)
+    if per:
+        out["hbm_bytes_per_view"] = round(sum(per.values()))
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
-    if main_k:
+    if per:
         with open(os.path.join(ROOT, "profiles", "pmc_main_kernel.json"), "w") as f:
-            json.dump({"tag": a.tag, "kernel": main_k[0],
-                       "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
-                       "fetch_bytes": kern[main_k[0]]["fetch_bytes"],
-                       "write_bytes": kern[main_k[0]]["write_bytes"]}, f, indent=1)
-    print(json.dumps(out, indent=1))
+            json.dump({"tag": a.tag, "kernel": a.kernel, "hbm_bytes_per_view": out["hbm_bytes_per_view"],
+                       "fetch_bytes_per_view": out.get("fetch_size_bytes_per_view"),
+                       "write_bytes_per_view": out.get("write_size_bytes_per_view")}, f, indent=1)
+    print(json.dumps({"trace": trace, "pmc": out}, indent=1))
 
 
 if __name__ == "__main__":
