@@ -120,7 +120,11 @@ __device__ inline uint32_t gray2bin_x2(uint32_t x) {
 // ------------------------------------------------------------------ stats kernel
 constexpr int kMaxBatch = 16;               // views per batched stats launch (blockIdx.y)
 constexpr int kStatsPx = 32;                // pixels per lane per stats iteration
-constexpr int kStatsBlocks = 64;            // stats workgroups per view (at most)
+constexpr int kStatsBlocks = 64;            // stats workgroups per view (at most), percentile path
+#ifndef SLG_STATS_OTSU_BLOCKS
+#define SLG_STATS_OTSU_BLOCKS 64                 // 128: 2.6% and 256: 10% slower bench (slot contention)
+#endif
+constexpr int kStatsBlocksOtsu = SLG_STATS_OTSU_BLOCKS;   // matrix-core Otsu path
 
 struct StatsParams {
   const uint8_t* white[kMaxBatch];
@@ -256,6 +260,56 @@ __device__ float percentile95_from_hist(const uint32_t* h, int64_t n) {
   return r;
 }
 
+// ---- Otsu histograms on the i8 matrix cores.  For 64 pixels v_k (k = 16 * lane-group + byte),
+// A[m][k] = [v_k >> 4 == m] and B[k][n] = [v_k & 15 == n], so one v_mfma_i32_16x16x64_i8 adds
+// the exact count of every value v = 16m + n: no LDS atomics (which retire about one lane per
+// clock), a few SWAR byte compares per lane instead.  Lane maps checked by
+// tools/mfma_hist_probe.hip; C/D: col = lane & 15, row = 4 * (lane >> 4) + r.
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+
+__device__ inline uint32_t eq_nib(uint32_t x, uint32_t rep) {   // bytes (< 16) equal -> 0x01
+  const uint32_t t = x ^ rep;
+  return (~((t | 0x80808080u) - 0x01010101u) >> 7) & 0x01010101u;
+}
+
+__device__ inline uint32_t sub_sat_u8x4(uint32_t w, uint32_t b) {   // per byte max(w - b, 0)
+  const uint32_t dl = ((w & 0x00ff00ffu) | 0x01000100u) - (b & 0x00ff00ffu);   // 256 + w - b
+  const uint32_t dh = (((w >> 8) & 0x00ff00ffu) | 0x01000100u) - ((b >> 8) & 0x00ff00ffu);
+  const uint32_t ml = ((dl >> 8) & 0x00010001u) * 0xffu, mh = ((dh >> 8) & 0x00010001u) * 0xffu;
+  return (dl & ml) | ((dh & mh) << 8);
+}
+
+// One wave adds 1024 pixels (16 per lane, pixel px_c + 16 * lane + byte) of white and of
+// clip(white - black) into its accumulators; `valid` = bytes of the chunk below n_px.
+__device__ inline void mfma_hist_chunk(const uint32_t (&w)[4], const uint32_t (&d)[4], int64_t px_c, int64_t n_px,
+                                       v4i32& acc_w, v4i32& acc_d) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t rep = uint32_t(lane & 15) * 0x01010101u;
+  const bool full = px_c + 1024 <= n_px;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int src = 4 * i + (lane >> 4);
+    v4i32 aw, bw, ad, bd;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t x = uint32_t(__shfl(int(w[q]), src));
+      const uint32_t y = uint32_t(__shfl(int(d[q]), src));
+      uint32_t vm = 0x01010101u;
+      if (!full) {
+        vm = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) vm |= (px_c + 16 * src + 4 * q + b < n_px ? 0x01u : 0u) << (8 * b);
+      }
+      aw[q] = int(eq_nib((x >> 4) & 0x0f0f0f0fu, rep) & vm);
+      bw[q] = int(eq_nib(x & 0x0f0f0f0fu, rep));
+      ad[q] = int(eq_nib((y >> 4) & 0x0f0f0f0fu, rep) & vm);
+      bd[q] = int(eq_nib(y & 0x0f0f0f0fu, rep));
+    }
+    acc_w = __builtin_amdgcn_mfma_i32_16x16x64_i8(aw, bw, acc_w, 0, 0, 0);
+    acc_d = __builtin_amdgcn_mfma_i32_16x16x64_i8(ad, bd, acc_d, 0, 0, 0);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   // 16 sub-histograms per kind (wave x lane&3), rows padded to 257 words so the copies of one
   // bin sit in different banks: a flat background costs at most 16-way same-address adds.
@@ -291,34 +345,53 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   __syncthreads();
 
   // hist kinds: otsu -> [0] white, [1] clip(white-black); percentile -> [0] black.
-  // Each lane takes kStatsPx consecutive pixels per step (all loads issued before use).
   const bool otsu = p.thresh_mode == SLG_THRESH_OTSU;
-  uint32_t* h0 = sh + (4 * wave + (tid & 3)) * 2 * kRow;
-  uint32_t* h1 = h0 + kRow;
-  uint32_t local_max = 0;
-  const int64_t per_block = int64_t(kBlock) * kStatsPx;
-  for (int64_t b0 = int64_t(blockIdx.x) * per_block; b0 < p.n_px; b0 += int64_t(gridDim.x) * per_block) {
-    const int64_t px0 = b0 + int64_t(tid) * kStatsPx;
-    uint2 w[kStatsPx / 8], b[kStatsPx / 8];
+  if (otsu) {                                  // matrix-core histograms (mfma_hist_chunk)
+    v4i32 acc_w = {0, 0, 0, 0}, acc_d = {0, 0, 0, 0};
+    const int lane = tid & 63;
+    const int64_t n_waves = int64_t(gridDim.x) * (kBlock / 64);
+    for (int64_t c = (int64_t(blockIdx.x) * (kBlock / 64) + wave) * 1024; c < p.n_px; c += n_waves * 1024) {
+      uint32_t w[4], d[4];
 #pragma unroll
-    for (int q = 0; q < kStatsPx / 8; ++q) {
-      const int64_t o = px0 + 8 * q < p.n_px ? px0 + 8 * q : 0;   // frames readable to round_up(n, 8)
-      w[q] = *reinterpret_cast<const uint2*>(white + o);
-      b[q] = *reinterpret_cast<const uint2*>(black + o);
+      for (int h = 0; h < 2; ++h) {            // 16 pixels per lane as two 8-byte loads
+        const int64_t o = c + 16 * lane + 8 * h;
+        const int64_t so = o < p.n_px ? o : 0;   // frames readable to round_up(n, 8)
+        const uint2 wq = *reinterpret_cast<const uint2*>(white + so);
+        const uint2 bq = *reinterpret_cast<const uint2*>(black + so);
+        w[2 * h] = wq.x; w[2 * h + 1] = wq.y;
+        d[2 * h] = sub_sat_u8x4(wq.x, bq.x); d[2 * h + 1] = sub_sat_u8x4(wq.y, bq.y);
+      }
+      mfma_hist_chunk(w, d, c, p.n_px, acc_w, acc_d);
     }
 #pragma unroll
-    for (int k = 0; k < kStatsPx; ++k) {
-      if (px0 + k >= p.n_px) break;
-      const uint2 wq = w[k >> 3], bq = b[k >> 3];
-      const int wv = (((k & 7) < 4 ? wq.x : wq.y) >> (8 * (k & 3))) & 0xff;
-      const int bv = (((k & 7) < 4 ? bq.x : bq.y) >> (8 * (k & 3))) & 0xff;
-      const int d = wv - bv;
-      if (otsu) {
-        atomicAdd(&h0[wv], 1u);
-        atomicAdd(&h1[d < 0 ? 0 : d], 1u);
-      } else {
+    for (int r = 0; r < 4; ++r) {              // wave sub-histograms: row-major bins 16*row + col
+      const int bin = 16 * (4 * (lane >> 4) + r) + (lane & 15);
+      if (acc_w[r]) atomicAdd(&sh[(2 * wave) * kRow + bin], uint32_t(acc_w[r]));
+      if (acc_d[r]) atomicAdd(&sh[(2 * wave + 1) * kRow + bin], uint32_t(acc_d[r]));
+    }
+  }
+  // percentile: LDS adds into 16 sub-histograms, kStatsPx consecutive pixels per lane and step
+  uint32_t local_max = 0;
+  if (!otsu) {
+    uint32_t* h0 = sh + (4 * wave + (tid & 3)) * 2 * kRow;
+    const int64_t per_block = int64_t(kBlock) * kStatsPx;
+    for (int64_t b0 = int64_t(blockIdx.x) * per_block; b0 < p.n_px; b0 += int64_t(gridDim.x) * per_block) {
+      const int64_t px0 = b0 + int64_t(tid) * kStatsPx;
+      uint2 w[kStatsPx / 8], b[kStatsPx / 8];
+#pragma unroll
+      for (int q = 0; q < kStatsPx / 8; ++q) {
+        const int64_t o = px0 + 8 * q < p.n_px ? px0 + 8 * q : 0;   // frames readable to round_up(n, 8)
+        w[q] = *reinterpret_cast<const uint2*>(white + o);
+        b[q] = *reinterpret_cast<const uint2*>(black + o);
+      }
+#pragma unroll
+      for (int k = 0; k < kStatsPx; ++k) {
+        if (px0 + k >= p.n_px) break;
+        const uint2 wq = w[k >> 3], bq = b[k >> 3];
+        const int wv = (((k & 7) < 4 ? wq.x : wq.y) >> (8 * (k & 3))) & 0xff;
+        const int bv = (((k & 7) < 4 ? bq.x : bq.y) >> (8 * (k & 3))) & 0xff;
         atomicAdd(&h0[bv], 1u);
-        local_max = max(local_max, uint32_t(d + 256));
+        local_max = max(local_max, uint32_t(wv - bv + 256));
       }
     }
   }
@@ -848,7 +921,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   constexpr int kIt = kTilePx / kB;        // 8 item rounds of one workgroup at most
   __shared__ uint32_t s_code[kTilePx];     // valid item: col | row << 16
   __shared__ uint32_t s_bgr[kTilePx];      // its BGR (24 bits)
-  __shared__ uint16_t s_off[kTilePx];      // its pixel offset inside the tile
+  __shared__ uint32_t s_uv[kTilePx];       // its pixel coordinates u | v << 16
   __shared__ int s_wtot[kB / 64];
   __shared__ int s_cnt[NS][kIt][kB / 64];  // kept points per (round, wave)
   __shared__ uint64_t s_excl[NS];
@@ -861,6 +934,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   const int64_t tile_px = int64_t(tile) * kTilePx;
   const int64_t px0 = tile_px + int64_t(tid) * kPx;
   const bool tail = tile == tiles - 1;               // block-uniform: guarded reads only here
+  const int tile_v0 = int(tile_px / p.width);
 
   // ------------------------------------------------------------ A: decode + tile compaction
   int n_items;
@@ -880,21 +954,23 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     const int2 sc = block_scan(__popc(valid), s_wtot);
     n_items = sc.y;
     int m = sc.x;
+    int u = int(tile_px - int64_t(tile_v0) * p.width) + tid * kPx, v = tile_v0;   // lane's first pixel
+    while (u >= p.width) { u -= p.width; ++v; }
 #pragma unroll
-    for (int k = 0; k < kPx; ++k)
+    for (int k = 0; k < kPx; ++k) {
       if (valid & (1u << k)) {
         s_code[m] = pack_code<ROW_MODE>(p, col[k], row[k]);
         s_bgr[m] = bgr_of(tex, k);
-        s_off[m] = uint16_t(tid * kPx + k);
+        s_uv[m] = uint32_t(u) | (uint32_t(v) << 16);
         ++m;
       }
+      if (++u == p.width) { u = 0; ++v; }
+    }
   }
   __syncthreads();
 
   // ------------------------------------------------------------ B: triangulate, balanced
   // Item m = tid + kB * i: every wave gets an equal share of the tile's valid pixels.
-  const int v0 = int(tile_px / p.width);
-  const int u0 = int(tile_px - int64_t(v0) * p.width);
   // Points stay in registers across the look-back (recomputing them after it instead frees
   // ~15 VGPRs for a fifth wave per SIMD but measured 6% slower).
   XT pts[NS][kIt][3];
@@ -906,9 +982,9 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     if (i * kB < n_items) {                          // block-uniform
       const int m = tid + kB * i;
       const bool in = m < n_items;
-      const uint32_t code = in ? s_code[m] : 0u;
-      int u = u0 + (in ? int(s_off[m]) : 0), v = v0;
-      while (u >= p.width) { u -= p.width; ++v; }
+      const uint32_t sc = s_code[m], suv = s_uv[m];   // read unconditionally (m < kTilePx) ...
+      const uint32_t code = in ? sc : 0u, uv = in ? suv : 0u;   // ... garbage past n_items masked
+      const int u = int(uv & 0xffffu), v = int(uv >> 16);
       uint32_t keep;
       if (p.dbg & 2) {                               // ablation: trivial triangulation
         keep = in ? (ROW_MODE == 2 ? 3u : 1u) : 0u;
@@ -1096,6 +1172,7 @@ int check_capture(const slg_capture* cap) {
   if (cap->height < 1 || cap->width < 1) return fail(SLG_ERR_INVALID, "bad image size %dx%d", cap->width, cap->height);
   const int64_t n_px = int64_t(cap->height) * cap->width;
   if (n_px >= (int64_t(1) << 31)) return fail(SLG_ERR_UNSUPPORTED, "image larger than 2^31 pixels");
+  if (cap->height > 65535 || cap->width > 65535) return fail(SLG_ERR_UNSUPPORTED, "image side above 65535 pixels");
   if (cap->frame_stride < ((n_px + 7) & ~int64_t(7)) || (cap->frame_stride & 7))
     return fail(SLG_ERR_INVALID, "frame_stride must be >= round_up(H*W, 8) and a multiple of 8");
   if (reinterpret_cast<uintptr_t>(cap->frames) & 7) return fail(SLG_ERR_INVALID, "frames must be 8-byte aligned");
@@ -1123,7 +1200,8 @@ int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* black
   // Few fat workgroups per view: each merges its sub-histograms into the view's histogram with
   // <= 512 global atomics, and a batch's stats pass takes few CU slots next to a fused launch.
   int64_t grid = (n_px + int64_t(kBlock) * kStatsPx - 1) / (int64_t(kBlock) * kStatsPx);
-  if (grid > kStatsBlocks) grid = kStatsBlocks;
+  const int64_t cap = sp.thresh_mode == SLG_THRESH_OTSU ? kStatsBlocksOtsu : kStatsBlocks;
+  if (grid > cap) grid = cap;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(stats_kernel, dim3(unsigned(grid), unsigned(n_views)), dim3(kBlock), 0, s, sp);
   return check_launch("stats_kernel");
