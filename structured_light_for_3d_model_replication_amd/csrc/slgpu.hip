@@ -67,6 +67,8 @@ struct WsHeader {
   double thr_s;            // float thresholds (for inspection / tests)
   double thr_c;
   int64_t totals[2];       // column / row stream point totals
+  uint64_t prof[6];        // SLG_DBG bit 6 (profiling): main3 phase time sums (100 MHz ticks):
+                           // A decode, B triangulate, C look-back, D stores; [4] workgroups
 };
 constexpr int kHistCopies = 16;            // partial histograms: blocks spread their atomics
 constexpr int64_t kHistPartOff = 8192;      // uint32 [kHistCopies][2][256] after the header
@@ -843,6 +845,9 @@ __global__ __launch_bounds__(kBlock) void decode_maps_kernel(MainParams p) {
 // 20 KB of LDS and no point staging keep several workgroups per CU resident, so one tile's
 // decode stream overlaps other tiles' fp64 work and look-back.
 constexpr int kMaxViews = 16;
+#ifndef SLG_VIEW_MAJOR
+#define SLG_VIEW_MAJOR 0                   // 1: all tiles of view 0 first, then view 1, ...
+#endif
 #ifndef SLG_M3_WAVES
 #define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
 #endif
@@ -928,13 +933,29 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = int(P.c.n_tiles);
+#if SLG_VIEW_MAJOR
   const int view = int(blockIdx.x) / tiles;          // grid = views x tiles, view-major
   const int tile = int(blockIdx.x) - view * tiles;
+#else
+  // Views interleaved in dispatch order: each view's look-back chain has only ~1/n_views of
+  // the resident workgroups in flight, so a tile waits on fewer, similar predecessors.
+  const int tile = int(blockIdx.x) / P.n_views;
+  const int view = int(blockIdx.x) - tile * P.n_views;
+#endif
   const MainParams p = view_params(P, view);
   const int64_t tile_px = int64_t(tile) * kTilePx;
   const int64_t px0 = tile_px + int64_t(tid) * kPx;
   const bool tail = tile == tiles - 1;               // block-uniform: guarded reads only here
   const int tile_v0 = int(tile_px / p.width);
+  const bool prof = (p.dbg & 64) != 0;               // phase timing (profiling builds of a run)
+  uint64_t t_phase = prof ? __builtin_amdgcn_s_memrealtime() : 0;
+  auto stamp = [&](int k) {
+    if (prof && tid == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(reinterpret_cast<unsigned long long*>(&P.v[0].ws->prof[k]), (unsigned long long)(t - t_phase));
+      t_phase = t;
+    }
+  };
 
   // ------------------------------------------------------------ A: decode + tile compaction
   int n_items;
@@ -969,6 +990,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   }
   __syncthreads();
 
+  stamp(0);
   // ------------------------------------------------------------ B: triangulate, balanced
   // Item m = tid + kB * i: every wave gets an equal share of the tile's valid pixels.
   // Points stay in registers across the look-back (recomputing them after it instead frees
@@ -1006,6 +1028,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   }
   __syncthreads();
 
+  stamp(1);
   // ------------------------------------------------------------ C: tile offset (look-back)
   if (wave == 0) {
 #pragma unroll 1
@@ -1035,6 +1058,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   }
   __syncthreads();
 
+  stamp(2);
   // ------------------------------------------------------------ D: ordered stores from registers
   if (p.dbg & 4) return;                             // ablation: no output stores
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1060,6 +1084,11 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       }
       base += round;
     }
+  }
+  if (prof) {
+    __syncthreads();
+    stamp(3);
+    if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&P.v[0].ws->prof[4]), 1ull);
   }
 }
 

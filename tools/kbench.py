@@ -105,6 +105,28 @@ def main():
             if name in res:
                 res[name]["per_view_us"] = round(res[name]["median_us"] / nb, 2)
                 print(name, "per view", res[name]["per_view_us"], file=sys.stderr, flush=True)
+    # phase timing of the fused kernel (SLG_DBG bit 6: per-workgroup s_memrealtime stamps)
+    if not want or "phases" in want:
+        nb = len(dfr)
+        beng = E.BatchReconstructor(H, W, nb)
+        bclouds = [E.Cloud(H * W, 1, False) for _ in range(nb)]
+        pb = beng.prepare(dfr, cfg, dcal, bclouds, 1)
+
+        def prof():
+            return np.frombuffer(beng.header(0, 0)[3136:3136 + 48].cpu().numpy().tobytes(), np.uint64).astype(np.float64)
+        os.environ["SLG_DBG"] = "64"
+        p0 = prof()
+        for _ in range(6):
+            beng.stats(pb)
+            beng.main(pb)
+        torch.cuda.synchronize()
+        d = prof() - p0
+        os.environ.pop("SLG_DBG")
+        wgs = max(d[4], 1.0)
+        ph = {k: round(d[i] / wgs * 0.01, 3) for i, k in enumerate(["A_decode", "B_tri", "C_lookback", "D_stores"])}
+        ph["workgroups"] = int(d[4])
+        res["phase_us_per_workgroup"] = ph
+        print("phase us per workgroup", ph, file=sys.stderr, flush=True)
     # pipelined: stats of batch k+1 on a side stream during batch k's fused launch
     nb = len(dfr)
     beng = E.BatchReconstructor(H, W, nb, slots=2)
