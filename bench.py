@@ -7,10 +7,12 @@ filter, tol 2.0), fp32 XYZ + BGR out.  Every step does the full path for its vie
 resident in HBM: the stats pass (histograms -> Otsu thresholds) and the fused
 decode/triangulate/compaction pass.  Steps rotate over a pool of distinct rendered turntable
 views (12 x 95 MB frame stacks > 256 MiB Infinity Cache) so frames stream from HBM.  Views are
-issued in batches (C3/C5 style): per batch of up to 16 views one batched stats launch and one
-fused main3 launch; the next batch's stats run on a side stream during this batch's fused
-launch (BatchReconstructor.run_pipelined; --pipeline serial: both on one stream,
-slg_reconstruct_batch).  One process per GPU (torchrun); each rank renders its own
+issued in batches (C3/C5 style): one fused main3 launch per batch of up to 16 views.  Default
+--pipeline fused: batch k's fused launch also computes batch k+2's Otsu histograms (per-tile
+partials) and a small kernel on a side stream turns them into thresholds beside batch k+1's
+launch; the first two batches of a run get a regular stats pass (BatchReconstructor.
+run_pipelined).  --pipeline overlap: a separate stats pass of batch k+1 on a side stream;
+--pipeline serial: stats + fused launch per batch on one stream (slg_reconstruct_batch).  One process per GPU (torchrun); each rank renders its own
 views (weak scaling, no data-path collective); value = all ranks' points / max-over-ranks time.
 
 Prints ONE JSON line on stdout (rank 0).  Diagnostics go to stderr.
@@ -71,12 +73,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=24)
-    ap.add_argument("--views", type=int, default=12, help="distinct rendered views in the pool")
+    ap.add_argument("--views", type=int, default=12, help="distinct rendered views")
+    ap.add_argument("--copies", type=int, default=3, help="device copies of each view in the pool")
     ap.add_argument("--batch", type=int, default=12, help="views per fused launch (<= 16)")
     ap.add_argument("--xyz", choices=["f32", "f64"], default="f32")
-    ap.add_argument("--pipeline", choices=["serial", "overlap"], default="overlap",
+    ap.add_argument("--pipeline", choices=["serial", "overlap", "fused"], default="fused",
                     help="serial: stats + fused launch per batch on one stream; overlap: the next "
-                         "batch's stats on a side stream during this batch's fused launch")
+                         "batch's stats on a side stream during this batch's fused launch; fused: "
+                         "batch k's fused launch computes batch k+2's histograms")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -105,7 +109,11 @@ def main():
 
     cfg = E.DecodeConfig(PW, PH, 11, 10, "otsu")
     row_mode, tol, f64 = 1, 2.0, args.xyz == "f64"
-    dframes = [E.DeviceFrames(list(v.frames), v.texture, device=dev) for v in views]
+    # Device pool: every rendered view uploaded `copies` times (distinct HBM buffers), so a batch
+    # never shares frames with the batch before or after next -- e.g. the histograms a fused
+    # launch computes for batch k+2 are cold HBM reads, as in a real turntable stream.
+    dframes = [E.DeviceFrames(list(v.frames), v.texture, device=dev) for _ in range(args.copies) for v in views]
+    P = len(dframes)
     dcal = E.DeviceCalib(cal, H, W, device=dev)
     B = max(1, min(args.batch, E.MAX_VIEWS_PER_LAUNCH))
     s_main = torch.cuda.Stream(device=dev)
@@ -118,14 +126,14 @@ def main():
         """Batch of n consecutive pool views from `start` on workspace/cloud slot `slot`."""
         key = (start, n, slot)
         if key not in preps:
-            fr = [dframes[(start + k) % len(views)] for k in range(n)]
+            fr = [dframes[(start + k) % P] for k in range(n)]
             preps[key] = beng.prepare(fr, cfg, dcal, clouds[slot][:n], row_mode, tol, slot=slot)
         return preps[key]
 
     # points per view: one sanity pass over the pool in batches of B (same launch shape as timed)
     pts = []
-    for v0 in range(0, len(views), B):
-        n = min(B, len(views) - v0)
+    for v0 in range(0, P, B):
+        n = min(B, P - v0)
         beng.run(prep(v0, n, 0), stream=s_main)
         s_main.synchronize()
         pts += [int(clouds[0][k].count.item()) for k in range(n)]
@@ -135,7 +143,7 @@ def main():
         out, j = [], 0
         while j < count:
             n = min(B, count - j)
-            out.append(prep((first + j) % len(views), n, len(out) % 2))
+            out.append(prep((first + j) % P, n, len(out) % 2))
             j += n
         return out
 
@@ -151,12 +159,12 @@ def main():
     frame_b = (2 + 2 * (11 + 10)) * H * W
     total_pts, bytes_alg = 0, 0.0
     for v in range(Wm, Wm + K):
-        total_pts += pts[v % len(views)]
-        bytes_alg += frame_b + out_b * pts[v % len(views)]
+        total_pts += pts[v % P]
+        bytes_alg += frame_b + out_b * pts[v % P]
 
     def run_all(batches, events=None):
-        if args.pipeline == "overlap":
-            beng.run_pipelined(batches, s_main, s_stats, events=events)
+        if args.pipeline in ("overlap", "fused"):
+            beng.run_pipelined(batches, s_main, s_stats, events=events, mode=args.pipeline)
         else:
             for k, pb in enumerate(batches):
                 beng.run(pb, events=None if events is None else events[k], stream=s_main)
@@ -221,7 +229,7 @@ def main():
             "config": {"workload": "C2: 1920x1080 view, 11 col + 10 row Gray bits + inverses + "
                                    "white/black (44 frames), Otsu, row_mode 1 tol 2.0, XYZ "
                                    f"{args.xyz} + BGR out",
-                       "views_per_rank": len(views), "points_per_view": int(np.mean(pts)),
+                       "views_per_rank": len(views), "device_pool": P, "points_per_view": int(np.mean(pts)),
                        "batch_views": B,
                        "launches": n_launch,
                        "stats_pipeline": args.pipeline,

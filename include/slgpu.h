@@ -184,6 +184,22 @@ int32_t slg_decode_triangulate_batch(const slg_capture *caps, int32_t n_views, c
                                      int64_t ws_stride, const slg_cloud *outs, void *const *timing_events,
                                      void *stream);
 
+/* Streaming turntable batches (thresh_mode OTSU only): the fused launch of batch k also
+ * computes the Otsu histograms of batch k+2 (`next`, n_next <= n_views views, same geometry),
+ * one 1 KB partial per 2048-pixel tile in each view's workspace slice; no separate pass over
+ * the white/black frames of batch k+2 is needed.  Batch k+2 must then use the SAME workspace
+ * slices as batch k, and slg_decode_stats_partials_batch on them (after this launch, before
+ * batch k+2's fused launch; it may overlap batch k+1's) turns the partials into thresholds and
+ * arms the slices for batch k+2.  Results are identical to slg_decode_stats_batch. */
+int32_t slg_decode_triangulate_batch_next(const slg_capture *caps, int32_t n_views,
+                                          const slg_decode_params *dp, const slg_calib *calib,
+                                          const slg_tri_params *tp, void *workspace, int64_t ws_stride,
+                                          const slg_cloud *outs, const slg_capture *next,
+                                          int32_t n_next, void *const *timing_events, void *stream);
+int32_t slg_decode_stats_partials_batch(int32_t n_views, int32_t height, int32_t width,
+                                        const slg_decode_params *dp, void *workspace,
+                                        int64_t ws_stride, void *stream);
+
 /* Count (into *mismatches, device int64) the Nc entries that differ bitwise from the cam_K
  * pinhole rays; 0 means SLG_RAYS_PINHOLE reproduces the table exactly. */
 int32_t slg_rays_match_pinhole(const double *rays, int32_t height, int32_t width, double fx,

@@ -82,7 +82,10 @@ __host__ __device__ inline int64_t n_state_words(int64_t n_px) { return 2 * n_ti
 __host__ __device__ inline int64_t states_bytes(int64_t n_px) { return align_up(n_state_words(n_px) * 8, 256); }
 __host__ __device__ inline int64_t scratch_xyz_off(int64_t n_px) { return kHeaderBytes + states_bytes(n_px); }
 __host__ __device__ inline int64_t scratch_bgr_off(int64_t n_px) { return scratch_xyz_off(n_px) + align_up(n_px * 24, 256); }
-__host__ __device__ inline int64_t ws_total(int64_t n_px) { return scratch_bgr_off(n_px) + align_up(n_px * 3, 256); }
+__host__ __device__ inline int64_t parts_off(int64_t n_px) { return scratch_bgr_off(n_px) + align_up(n_px * 3, 256); }
+// per tile: the Otsu histograms of the batch after next over the tile's pixels, u16 [2][256]
+constexpr int64_t kPartWords = 256;         // packed u16 pairs per tile
+__host__ __device__ inline int64_t ws_total(int64_t n_px) { return parts_off(n_px) + align_up(n_tiles_of(n_px) * kPartWords * 4, 256); }
 
 // ------------------------------------------------------------------ small helpers
 __device__ inline uint64_t ld_state(const uint64_t* p) {
@@ -127,6 +130,7 @@ constexpr int kStatsBlocks = 64;            // stats workgroups per view (at mos
 #define SLG_STATS_OTSU_BLOCKS 64                 // 128: 2.6% and 256: 10% slower bench (slot contention)
 #endif
 constexpr int kStatsBlocksOtsu = SLG_STATS_OTSU_BLOCKS;   // matrix-core Otsu path
+constexpr int kStatsPartBlocks = 16;        // partials mode: workgroups per view
 
 struct StatsParams {
   const uint8_t* white[kMaxBatch];
@@ -139,6 +143,10 @@ struct StatsParams {
   double shadow_val;
   double contrast_val;
   int32_t dbg;             // profiling ablation (SLG_DBG bit 4: skip the Otsu tail)
+  int32_t pad2;
+  const uint32_t* parts[kMaxBatch];   // Otsu from per-tile partial histograms (NULL: from frames)
+  int64_t n_parts;                    // tiles per view
+  int64_t pad_zero;                   // zero pixels counted past n_px (removed from bin 0)
 };
 
 // a / b correctly rounded from y = RN(1/b) (Markstein): with y correctly rounded and q1
@@ -159,10 +167,13 @@ __device__ inline bool div_rn_ok(double a) {
 // OpenCV getThreshVal_Otsu_8u (see oracle/sl_oracle.py:otsu_from_hist) evaluated by one wave.
 // Bit-exact with the sequential fp64 loop: only order-independent pieces run in parallel.
 //  * mu = sum(i*h[i]) of exact integers (< 2^53) == OpenCV's sequential double sum;
-//  * q1 (running sum of p_i = h[i]*scale) and mu1 (mu1 = (mu1*q1_prev + i*p_i)/q1) are one
-//    fused sequential chain on wave-uniform registers (v_readlane of the bin's p_i, results
-//    kept by the owning lane); bins that OpenCV skips cost no division, and the chain
-//    stops once q1 > 1-FLT_EPSILON (every later bin is skipped);
+//  * q1 (running sum of p_i = h[i]*scale) is one sequential add chain (same rounding as the
+//    loop); it alone decides which bins OpenCV skips, so the skip flags, i*p_i and
+//    y = RN(1/q1) are then computed lane-parallel, bin i on lane i/4;
+//  * the remaining chain mu1 = (mu1*q1_prev + i*p_i)/q1 runs on wave-uniform registers up to
+//    the last unskipped bin, each division as the Markstein pair div_rn(., q1, y) (IEEE
+//    division when div_rn_ok refuses the numerator): 7 dependent fp64 ops per bin instead of a
+//    full IEEE division sequence;
 //  * sigma per bin and the first-maximum argmax (strict '>' from 0) are lane-parallel.
 __device__ inline double readlane_f64(double v, int l) {
   const uint64_t b = uint64_t(__double_as_longlong(v));
@@ -175,38 +186,50 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
   const int lane = threadIdx.x & 63;
   const double scale = 1.0 / double(n);
   const double eps = double(__FLT_EPSILON__);
-  double pv[4], q1r[4], m1r[4];
-  uint32_t okr = 0;                                  // bit j: bin 4*lane+j not skipped
+  double pv[4], ip[4], q1r[4], qpr[4], yr[4], m1r[4];
   uint64_t isum = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int i = 4 * lane + j;
     pv[j] = double(h[i]) * scale;
+    ip[j] = double(i) * pv[j];
     isum += uint64_t(i) * h[i];
-    q1r[j] = 0.0;
-    m1r[j] = 0.0;
+    q1r[j] = qpr[j] = yr[j] = m1r[j] = 0.0;
   }
   isum = wave_sum(isum);
   const double mu = double(isum) * scale;
-  double q1 = 0.0, mu1 = 0.0;
+  double q1 = 0.0;                                   // 1. the q1 chain (OpenCV's order)
   for (int l = 0; l < 64; ++l) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const double p_i = readlane_f64(pv[j], l);
-      mu1 *= q1;                                     // mu1 *= q1 (previous q1)
-      q1 += p_i;
-      const double q2 = 1.0 - q1;
-      const int skip = __builtin_amdgcn_readfirstlane(int(fmin(q1, q2) < eps || fmax(q1, q2) > 1.0 - eps));
-      if (!skip) {
-        mu1 = (mu1 + double(4 * l + j) * p_i) / q1;
-        if (lane == l) {                             // results back to the bin's lane
-          q1r[j] = q1;
-          m1r[j] = mu1;
-          okr |= 1u << j;
-        }
+      const double nq = q1 + readlane_f64(pv[j], l);
+      if (lane == l) { qpr[j] = q1; q1r[j] = nq; }
+      q1 = nq;
+    }
+  }
+  uint32_t okr = 0;                                  // 2. bit j: bin 4*lane+j not skipped
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const double q2 = 1.0 - q1r[j];
+    if (!(fmin(q1r[j], q2) < eps || fmax(q1r[j], q2) > 1.0 - eps)) {
+      okr |= 1u << j;
+      yr[j] = 1.0 / q1r[j];
+    }
+  }
+  const int l_end = 64 - __builtin_clzll(__ballot(okr != 0) | 1ull);   // lanes with work: [0, l_end)
+  double mu1 = 0.0;                                  // 3. the mu1 chain
+  for (int l = 0; l < l_end; ++l) {
+    const uint32_t okl = __builtin_amdgcn_readlane(okr, l);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mu1 *= readlane_f64(qpr[j], l);                // mu1 *= q1 (previous q1)
+      if (okl & (1u << j)) {
+        const double a = mu1 + readlane_f64(ip[j], l);
+        const double q = readlane_f64(q1r[j], l);
+        mu1 = div_rn_ok(a) ? div_rn(a, q, readlane_f64(yr[j], l)) : a / q;
+        if (lane == l) m1r[j] = mu1;
       }
     }
-    if (__builtin_amdgcn_readfirstlane(int(q1 > 1.0 - eps))) break;   // all later bins skipped
   }
   double best = 0.0;
   int best_i = INT_MAX;
@@ -263,16 +286,17 @@ __device__ float percentile95_from_hist(const uint32_t* h, int64_t n) {
 }
 
 // ---- Otsu histograms on the i8 matrix cores.  For 64 pixels v_k (k = 16 * lane-group + byte),
-// A[m][k] = [v_k >> 4 == m] and B[k][n] = [v_k & 15 == n], so one v_mfma_i32_16x16x64_i8 adds
-// the exact count of every value v = 16m + n: no LDS atomics (which retire about one lane per
-// clock), a few SWAR byte compares per lane instead.  Lane maps checked by
+// A[m][k] = 16 * [v_k >> 4 == m] and B[k][n] = 16 * [v_k & 15 == n], so one
+// v_mfma_i32_16x16x64_i8 adds 256 x the count of every value v = 16m + n: no LDS atomics (which
+// retire about one lane per clock).  Each lane splits its 16 pixels into hi / lo nibble planes
+// once and stages them in wave-private LDS; an MFMA step then reads its 64 pixels with four
+// broadcast ds_read_b128 (16 lanes share an address) and builds each operand dword in two VALU
+// ops: ((nib ^ (m ^ 15)) + 1) & 0x10 = 16 - (nib ^ m) masked to bit 4, i.e. 0x10 iff nib == m
+// (no carries between bytes: every byte stays in 1..16).  Lane maps checked by
 // tools/mfma_hist_probe.hip; C/D: col = lane & 15, row = 4 * (lane >> 4) + r.
 typedef int v4i32 __attribute__((ext_vector_type(4)));
-
-__device__ inline uint32_t eq_nib(uint32_t x, uint32_t rep) {   // bytes (< 16) equal -> 0x01
-  const uint32_t t = x ^ rep;
-  return (~((t | 0x80808080u) - 0x01010101u) >> 7) & 0x01010101u;
-}
+constexpr int kHistChunk = 1024;            // pixels per wave and MFMA chunk (16 per lane)
+constexpr int64_t kHistMaxChunks = 8000;    // per wave: 8000 * 1024 * 256 < 2^31 (i32 accumulators)
 
 __device__ inline uint32_t sub_sat_u8x4(uint32_t w, uint32_t b) {   // per byte max(w - b, 0)
   const uint32_t dl = ((w & 0x00ff00ffu) | 0x01000100u) - (b & 0x00ff00ffu);   // 256 + w - b
@@ -281,34 +305,54 @@ __device__ inline uint32_t sub_sat_u8x4(uint32_t w, uint32_t b) {   // per byte 
   return (dl & ml) | ((dh & mh) << 8);
 }
 
-// One wave adds 1024 pixels (16 per lane, pixel px_c + 16 * lane + byte) of white and of
-// clip(white - black) into its accumulators; `valid` = bytes of the chunk below n_px.
-__device__ inline void mfma_hist_chunk(const uint32_t (&w)[4], const uint32_t (&d)[4], int64_t px_c, int64_t n_px,
+__device__ inline int onehot16(uint32_t nib, uint32_t repx) {      // bytes: 0x10 iff nib == m
+  return int(((nib ^ repx) + 0x01010101u) & 0x10101010u);
+}
+
+// One wave adds 1024 pixels (pixel c + 16 * lane + byte: white w[], clip(white - black) d[])
+// into its accumulators.  `stage` = this wave's 4 x 64 uint4 of LDS.
+__device__ inline void mfma_hist_chunk(uint4* stage, const uint32_t (&w)[4], const uint32_t (&d)[4],
                                        v4i32& acc_w, v4i32& acc_d) {
   const int lane = threadIdx.x & 63;
-  const uint32_t rep = uint32_t(lane & 15) * 0x01010101u;
-  const bool full = px_c + 1024 <= n_px;
+  const uint32_t m4 = 0x0f0f0f0fu;
+  stage[lane] = make_uint4((w[0] >> 4) & m4, (w[1] >> 4) & m4, (w[2] >> 4) & m4, (w[3] >> 4) & m4);
+  stage[64 + lane] = make_uint4(w[0] & m4, w[1] & m4, w[2] & m4, w[3] & m4);
+  stage[128 + lane] = make_uint4((d[0] >> 4) & m4, (d[1] >> 4) & m4, (d[2] >> 4) & m4, (d[3] >> 4) & m4);
+  stage[192 + lane] = make_uint4(d[0] & m4, d[1] & m4, d[2] & m4, d[3] & m4);
+  // same-wave LDS accesses complete in order: no barrier between these writes and the reads
+  const uint32_t repx = (uint32_t(lane & 15) * 0x01010101u) ^ m4;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int src = 4 * i + (lane >> 4);
-    v4i32 aw, bw, ad, bd;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t x = uint32_t(__shfl(int(w[q]), src));
-      const uint32_t y = uint32_t(__shfl(int(d[q]), src));
-      uint32_t vm = 0x01010101u;
-      if (!full) {
-        vm = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) vm |= (px_c + 16 * src + 4 * q + b < n_px ? 0x01u : 0u) << (8 * b);
-      }
-      aw[q] = int(eq_nib((x >> 4) & 0x0f0f0f0fu, rep) & vm);
-      bw[q] = int(eq_nib(x & 0x0f0f0f0fu, rep));
-      ad[q] = int(eq_nib((y >> 4) & 0x0f0f0f0fu, rep) & vm);
-      bd[q] = int(eq_nib(y & 0x0f0f0f0fu, rep));
-    }
+    const uint4 hw = stage[src], lw = stage[64 + src], hd = stage[128 + src], ld = stage[192 + src];
+    const v4i32 aw = {onehot16(hw.x, repx), onehot16(hw.y, repx), onehot16(hw.z, repx), onehot16(hw.w, repx)};
+    const v4i32 bw = {onehot16(lw.x, repx), onehot16(lw.y, repx), onehot16(lw.z, repx), onehot16(lw.w, repx)};
+    const v4i32 ad = {onehot16(hd.x, repx), onehot16(hd.y, repx), onehot16(hd.z, repx), onehot16(hd.w, repx)};
+    const v4i32 bd = {onehot16(ld.x, repx), onehot16(ld.y, repx), onehot16(ld.z, repx), onehot16(ld.w, repx)};
     acc_w = __builtin_amdgcn_mfma_i32_16x16x64_i8(aw, bw, acc_w, 0, 0, 0);
     acc_d = __builtin_amdgcn_mfma_i32_16x16x64_i8(ad, bd, acc_d, 0, 0, 0);
+  }
+}
+
+// 16 pixels of white and clip(white - black) for lane `lane` of the chunk at c; bytes at or
+// past n_px read as 0 (the last arriver removes them from bin 0).
+__device__ inline void hist_load(const uint8_t* white, const uint8_t* black, int64_t c, int64_t n_px,
+                                 uint32_t (&w)[4], uint32_t (&d)[4]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {             // two 8-byte loads
+    const int64_t o = c + 16 * lane + 8 * h;
+    const int64_t so = o < n_px ? o : 0;    // frames readable to round_up(n, 8)
+    uint2 wq = *reinterpret_cast<const uint2*>(white + so);
+    uint2 bq = *reinterpret_cast<const uint2*>(black + so);
+    if (o + 8 > n_px) {                     // tail: zero the bytes at or past n_px
+      const int64_t keep = n_px - o;        // <= 0: none
+      const uint64_t mk = keep <= 0 ? 0 : (~0ull >> (64 - 8 * keep));
+      wq.x &= uint32_t(mk); wq.y &= uint32_t(mk >> 32);
+      bq.x &= uint32_t(mk); bq.y &= uint32_t(mk >> 32);
+    }
+    w[2 * h] = wq.x; w[2 * h + 1] = wq.y;
+    d[2 * h] = sub_sat_u8x4(wq.x, bq.x); d[2 * h + 1] = sub_sat_u8x4(wq.y, bq.y);
   }
 }
 
@@ -317,6 +361,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   // bin sit in different banks: a flat background costs at most 16-way same-address adds.
   constexpr int kRow = 257;
   __shared__ uint32_t sh[16 * 2 * kRow];
+  __shared__ uint4 s_stage[(kBlock / 64) * 256];   // Otsu: per wave hi/lo nibble planes of w, d
   __shared__ uint32_t s_maxd;
   __shared__ uint32_t s_last;
   const int tid = threadIdx.x;
@@ -348,28 +393,42 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
 
   // hist kinds: otsu -> [0] white, [1] clip(white-black); percentile -> [0] black.
   const bool otsu = p.thresh_mode == SLG_THRESH_OTSU;
-  if (otsu) {                                  // matrix-core histograms (mfma_hist_chunk)
+  if (otsu && p.parts[view]) {                 // partials of a fused launch: thread t owns bins 2t, 2t+1
+    const uint32_t* pp = p.parts[view];
+    const int64_t per = (p.n_parts + gridDim.x - 1) / gridDim.x;
+    const int64_t t0 = int64_t(blockIdx.x) * per, t1 = t0 + per < p.n_parts ? t0 + per : p.n_parts;
+    uint32_t a0 = 0, a1 = 0;
+#pragma unroll 8
+    for (int64_t k = t0; k < t1; ++k) {
+      const uint32_t v = pp[k * kPartWords + tid];
+      a0 += v & 0xffffu;
+      a1 += v >> 16;
+    }
+    const int i0 = 2 * tid;                    // [white 0..255 | clip 256..511]
+    sh[(i0 >> 8) * kRow + (i0 & 255)] = a0;
+    sh[(i0 >> 8) * kRow + (i0 & 255) + 1] = a1;
+  } else if (otsu) {                           // matrix-core histograms (mfma_hist_chunk)
     v4i32 acc_w = {0, 0, 0, 0}, acc_d = {0, 0, 0, 0};
     const int lane = tid & 63;
-    const int64_t n_waves = int64_t(gridDim.x) * (kBlock / 64);
-    for (int64_t c = (int64_t(blockIdx.x) * (kBlock / 64) + wave) * 1024; c < p.n_px; c += n_waves * 1024) {
-      uint32_t w[4], d[4];
+    const int64_t step = int64_t(gridDim.x) * (kBlock / 64) * kHistChunk;
+    int64_t c = (int64_t(blockIdx.x) * (kBlock / 64) + wave) * kHistChunk;
+    uint32_t w[4], d[4];
+    if (c < p.n_px) hist_load(white, black, c, p.n_px, w, d);
+    for (; c < p.n_px; c += step) {            // next chunk's loads in flight during the MFMAs
+      uint32_t wn[4], dn[4];
+      const bool more = c + step < p.n_px;
+      if (more) hist_load(white, black, c + step, p.n_px, wn, dn);
+      mfma_hist_chunk(s_stage + wave * 256, w, d, acc_w, acc_d);
+      if (more) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {            // 16 pixels per lane as two 8-byte loads
-        const int64_t o = c + 16 * lane + 8 * h;
-        const int64_t so = o < p.n_px ? o : 0;   // frames readable to round_up(n, 8)
-        const uint2 wq = *reinterpret_cast<const uint2*>(white + so);
-        const uint2 bq = *reinterpret_cast<const uint2*>(black + so);
-        w[2 * h] = wq.x; w[2 * h + 1] = wq.y;
-        d[2 * h] = sub_sat_u8x4(wq.x, bq.x); d[2 * h + 1] = sub_sat_u8x4(wq.y, bq.y);
+        for (int q = 0; q < 4; ++q) { w[q] = wn[q]; d[q] = dn[q]; }
       }
-      mfma_hist_chunk(w, d, c, p.n_px, acc_w, acc_d);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {              // wave sub-histograms: row-major bins 16*row + col
       const int bin = 16 * (4 * (lane >> 4) + r) + (lane & 15);
-      if (acc_w[r]) atomicAdd(&sh[(2 * wave) * kRow + bin], uint32_t(acc_w[r]));
-      if (acc_d[r]) atomicAdd(&sh[(2 * wave + 1) * kRow + bin], uint32_t(acc_d[r]));
+      if (acc_w[r]) atomicAdd(&sh[(2 * wave) * kRow + bin], uint32_t(acc_w[r]) >> 8);
+      if (acc_d[r]) atomicAdd(&sh[(2 * wave + 1) * kRow + bin], uint32_t(acc_d[r]) >> 8);
     }
   }
   // percentile: LDS adds into 16 sub-histograms, kStatsPx consecutive pixels per lane and step
@@ -433,6 +492,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
 #pragma unroll
     for (int c = 0; c < kHistCopies; ++c)
       acc += __hip_atomic_load(hist_part + c * 512 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (otsu && (i & 255) == 0) acc -= uint32_t(p.pad_zero);   // zero padding past n_px
     hg[i] = acc;
   }
   if (tid == 0) s_maxd = __hip_atomic_load(&ws->max_diff_enc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -868,6 +928,9 @@ struct ViewIO {
   int64_t stride;             // frame stride of this view
   int32_t col_first, col_pairs, col_pre, col_post;   // decode plan of this view (frames present)
   int32_t row_first, row_pairs, row_pre, row_post;
+  const uint8_t* hn_white;    // batch after next: white / black of the view in this slot, whose
+  const uint8_t* hn_black;    // Otsu histograms this launch computes per tile (NULL: none)
+  uint32_t* hn_part;          // -> [n_tiles][kPartWords] of this view's workspace slice
 };
 
 struct Main3Params {
@@ -876,6 +939,8 @@ struct Main3Params {
   int32_t pad;
   ViewIO v[kMaxViews];
 };
+
+static_assert(sizeof(Main3Params) <= 4096, "kernel arguments");
 
 __device__ inline MainParams view_params(const Main3Params& P, int view) {
   MainParams q = P.c;
@@ -896,6 +961,72 @@ __device__ inline uint32_t bgr_of(const uint32_t (&t)[6], int k) {
   const int b = 3 * k, w = b >> 2, s = 8 * (b & 3);
   const uint64_t pair = uint64_t(t[w]) | (uint64_t(w + 1 < 6 ? t[w + 1] : 0u) << 32);
   return uint32_t(pair >> s) & 0xffffffu;
+}
+
+// The Otsu histograms (white, clip(white - black)) of another capture over this tile's pixel
+// range, as u16 counts [2][256] packed in pairs (1 KB per tile) -- the stats pass of the batch
+// after next, carried by this fused launch (stats_kernel's partials mode sums the tiles).
+// Split so it costs neither latency nor chain time: the loads are issued when the workgroup
+// starts (hist_next_load), the nibble planes staged once the points are computed
+// (hist_next_stage), the matrix-core counting done by waves 1..3 while wave 0 runs the
+// look-back (hist_next_count, as mfma_hist_chunk) and the partial written after it
+// (hist_next_write).  Bytes past n_px count as 0 (pad_zero).
+__device__ inline void hist_next_load(const uint8_t* white, const uint8_t* black, int64_t n_px, int64_t o,
+                                      uint2& wq, uint2& bq) {
+  wq = make_uint2(0, 0);
+  bq = make_uint2(0, 0);
+  if (o < n_px) {                            // frames readable to round_up(n, 8)
+    wq = *reinterpret_cast<const uint2*>(white + o);
+    bq = *reinterpret_cast<const uint2*>(black + o);
+  }
+}
+
+// stage: [wave][hi_w, lo_w, hi_d, lo_d][64 lanes] uint2 (the lane's 8 pixels per plane)
+__device__ inline void hist_next_stage(uint2 wq, uint2 bq, int64_t n_px, int64_t o, uint2* stage) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (o + 8 > n_px) {                        // tail: zero the bytes at or past n_px
+    const uint64_t mk = o >= n_px ? 0ull : (~0ull >> (64 - 8 * (n_px - o)));
+    wq.x &= uint32_t(mk); wq.y &= uint32_t(mk >> 32);
+    bq.x &= uint32_t(mk); bq.y &= uint32_t(mk >> 32);
+  }
+  const uint32_t m4 = 0x0f0f0f0fu;
+  const uint32_t d0 = sub_sat_u8x4(wq.x, bq.x), d1 = sub_sat_u8x4(wq.y, bq.y);
+  uint2* st = stage + wave * 256;
+  st[lane] = make_uint2((wq.x >> 4) & m4, (wq.y >> 4) & m4);
+  st[64 + lane] = make_uint2(wq.x & m4, wq.y & m4);
+  st[128 + lane] = make_uint2((d0 >> 4) & m4, (d1 >> 4) & m4);
+  st[192 + lane] = make_uint2(d0 & m4, d1 & m4);
+}
+
+// Steps h, h + n_help, ... of the tile's kTilePx / 64 MFMA steps (64 pixels each), added to
+// s_h[512] (zeroed beforehand) with LDS atomics.
+__device__ inline void hist_next_count(const uint2* stage, uint32_t* s_h, int h, int n_help) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t repx = (uint32_t(lane & 15) * 0x01010101u) ^ 0x0f0f0f0fu;
+  v4i32 acc_w = {0, 0, 0, 0}, acc_d = {0, 0, 0, 0};
+  for (int step = h; step < kTilePx / 64; step += n_help) {
+    const uint2* st = stage + (step >> 3) * 256 + 8 * (step & 7) + 2 * (lane >> 4);   // lanes src, src+1
+    const uint4 hw = *reinterpret_cast<const uint4*>(st);
+    const uint4 lw = *reinterpret_cast<const uint4*>(st + 64);
+    const uint4 hd = *reinterpret_cast<const uint4*>(st + 128);
+    const uint4 ld = *reinterpret_cast<const uint4*>(st + 192);
+    const v4i32 aw = {onehot16(hw.x, repx), onehot16(hw.y, repx), onehot16(hw.z, repx), onehot16(hw.w, repx)};
+    const v4i32 bw = {onehot16(lw.x, repx), onehot16(lw.y, repx), onehot16(lw.z, repx), onehot16(lw.w, repx)};
+    const v4i32 ad = {onehot16(hd.x, repx), onehot16(hd.y, repx), onehot16(hd.z, repx), onehot16(hd.w, repx)};
+    const v4i32 bd = {onehot16(ld.x, repx), onehot16(ld.y, repx), onehot16(ld.z, repx), onehot16(ld.w, repx)};
+    acc_w = __builtin_amdgcn_mfma_i32_16x16x64_i8(aw, bw, acc_w, 0, 0, 0);
+    acc_d = __builtin_amdgcn_mfma_i32_16x16x64_i8(ad, bd, acc_d, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int bin = 16 * (4 * (lane >> 4) + r) + (lane & 15);
+    if (acc_w[r]) atomicAdd(&s_h[bin], uint32_t(acc_w[r]) >> 8);
+    if (acc_d[r]) atomicAdd(&s_h[256 + bin], uint32_t(acc_d[r]) >> 8);
+  }
+}
+
+__device__ inline void hist_next_write(const uint32_t* s_h, uint32_t* part) {
+  for (int i = threadIdx.x; i < kPartWords; i += kTileBlock) part[i] = s_h[2 * i] | (s_h[2 * i + 1] << 16);
 }
 
 // Block-wide exclusive scan of one int per lane: (exclusive prefix, block total).
@@ -930,6 +1061,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   __shared__ int s_wtot[kB / 64];
   __shared__ int s_cnt[NS][kIt][kB / 64];  // kept points per (round, wave)
   __shared__ uint64_t s_excl[NS];
+  __shared__ __attribute__((aligned(16))) uint2 s_hstage[(kB / 64) * 256];   // next-batch nibble planes
+  __shared__ uint32_t s_hn[512];                                             // next-batch histograms
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = int(P.c.n_tiles);
@@ -957,6 +1090,13 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     }
   };
 
+  // stats pass of the batch after next (hist_next_*): loads now, counting during phase C
+  const bool hn = P.v[view].hn_part != nullptr;     // block-uniform
+  uint2 hn_w, hn_b;
+  if (hn) {
+    hist_next_load(P.v[view].hn_white, P.v[view].hn_black, p.n_px, px0, hn_w, hn_b);
+    for (int i = tid; i < 512; i += kB) s_hn[i] = 0;   // ordered before phase C by block_scan's barrier
+  }
   // ------------------------------------------------------------ A: decode + tile compaction
   int n_items;
   {
@@ -1026,6 +1166,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       for (int s = 0; s < NS; ++s) s_cnt[s][i][wave] = __popcll(km[s][i]);
     }
   }
+  if (hn) hist_next_stage(hn_w, hn_b, p.n_px, px0, s_hstage);
   __syncthreads();
 
   stamp(1);
@@ -1055,8 +1196,11 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
         }
       }
     }
+  } else if (hn) {                                   // waves 1..: next-batch histograms meanwhile
+    hist_next_count(s_hstage, s_hn, wave - 1, kB / 64 - 1);
   }
   __syncthreads();
+  if (hn) hist_next_write(s_hn, P.v[view].hn_part + int64_t(tile) * kPartWords);
 
   stamp(2);
   // ------------------------------------------------------------ D: ordered stores from registers
@@ -1212,14 +1356,20 @@ int debug_flags();
 
 // One stats launch for n_views views (<= kMaxBatch) of one geometry; view v reads white/black
 // from whites[v] / blacks[v] and owns the workspace slice at workspace + v * ws_stride.
+// from_parts: Otsu from the per-tile partial histograms in each slice (written by a fused
+// launch's next-batch pass) instead of from white/black frames.
 int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* blacks, int n_views, int64_t n_px,
-                       const slg_decode_params* dp, char* workspace, int64_t ws_stride, hipStream_t s) {
+                       const slg_decode_params* dp, char* workspace, int64_t ws_stride, hipStream_t s,
+                       bool from_parts = false) {
   StatsParams sp{};
   for (int v = 0; v < n_views; ++v) {
     sp.white[v] = whites ? whites[v] : nullptr;
     sp.black[v] = blacks ? blacks[v] : nullptr;
     sp.wsv[v] = reinterpret_cast<WsHeader*>(workspace + int64_t(v) * ws_stride);
+    if (from_parts) sp.parts[v] = reinterpret_cast<const uint32_t*>(workspace + int64_t(v) * ws_stride + parts_off(n_px));
   }
+  sp.n_parts = n_tiles_of(n_px);
+  sp.pad_zero = from_parts ? sp.n_parts * kTilePx - n_px : align_up(n_px, kHistChunk) - n_px;
   sp.n_px = n_px;
   sp.n_state_words = n_state_words(n_px);
   sp.thresh_mode = dp ? dp->thresh_mode : SLG_THRESH_MANUAL;
@@ -1231,6 +1381,12 @@ int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* black
   int64_t grid = (n_px + int64_t(kBlock) * kStatsPx - 1) / (int64_t(kBlock) * kStatsPx);
   const int64_t cap = sp.thresh_mode == SLG_THRESH_OTSU ? kStatsBlocksOtsu : kStatsBlocks;
   if (grid > cap) grid = cap;
+  if (sp.thresh_mode == SLG_THRESH_OTSU) {   // bound chunks per wave (i32 MFMA accumulators)
+    const int64_t per_block = int64_t(kBlock / 64) * kHistChunk * kHistMaxChunks;
+    const int64_t need = (n_px + per_block - 1) / per_block;
+    if (grid < need) grid = need;
+  }
+  if (from_parts) grid = sp.n_parts < kStatsPartBlocks ? sp.n_parts : kStatsPartBlocks;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(stats_kernel, dim3(unsigned(grid), unsigned(n_views)), dim3(kBlock), 0, s, sp);
   return check_launch("stats_kernel");
@@ -1349,10 +1505,22 @@ int check_batch(const slg_capture* caps, int n_views) {
 // slice): one main3 launch per kMaxViews views.  timing_events: 2 per launch, or NULL.
 int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* dp, const slg_calib* calib,
                 const slg_tri_params* tp, char* ws, int64_t ws_stride, const slg_cloud* outs,
-                void* const* timing_events, hipStream_t s) {
+                void* const* timing_events, hipStream_t s, const slg_capture* next = nullptr, int n_next = 0) {
   if (!caps || n_views < 1 || !dp || !ws || !outs) return fail(SLG_ERR_INVALID, "NULL argument");
   int rc = check_batch(caps, n_views);
   if (rc) return rc;
+  if (n_next) {                                     // the batch after next rides along (Otsu only)
+    if (!next || n_next < 0 || n_next > n_views) return fail(SLG_ERR_INVALID, "next batch: NULL or more views than this batch");
+    if (dp->thresh_mode != SLG_THRESH_OTSU) return fail(SLG_ERR_UNSUPPORTED, "next-batch histograms need thresh_mode OTSU");
+    for (int v = 0; v < n_next; ++v) {
+      rc = check_capture(&next[v]);
+      if (rc) return rc;
+      if (next[v].n_frames < 4)
+        return fail(SLG_ERR_NOT_ENOUGH, "Not enough images (got %d, need at least 4).", next[v].n_frames);
+      if (next[v].height != caps[0].height || next[v].width != caps[0].width)
+        return fail(SLG_ERR_INVALID, "next batch must share this batch's geometry");
+    }
+  }
   for (int v = 0; v < n_views; ++v) {
     rc = make_plan(&caps[v], dp, nullptr);
     if (rc) return rc;
@@ -1380,6 +1548,11 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
       make_plan(&caps[v], dp, &pl);
       io.col_first = pl.col_first; io.col_pairs = pl.col_pairs; io.col_pre = pl.col_pre; io.col_post = pl.col_post;
       io.row_first = pl.row_first; io.row_pairs = pl.row_pairs; io.row_pre = pl.row_pre; io.row_post = pl.row_post;
+      if (v < n_next) {
+        io.hn_white = next[v].frames;
+        io.hn_black = next[v].frames + next[v].frame_stride;
+        io.hn_part = reinterpret_cast<uint32_t*>(ws + int64_t(v) * ws_stride + parts_off(n_px));
+      }
     }
     if (timing_events && timing_events[2 * launch]) hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * launch]), s);
     rc = launch_main3(fn, mp, tp, &outs[v0], s);
@@ -1645,6 +1818,31 @@ int32_t slg_decode_triangulate_batch(const slg_capture* caps, int32_t n_views, c
                                      void* stream) {
   return fused_batch(caps, n_views, dp, calib, tp, static_cast<char*>(workspace), ws_stride, outs, timing_events,
                      static_cast<hipStream_t>(stream));
+}
+
+int32_t slg_decode_triangulate_batch_next(const slg_capture* caps, int32_t n_views, const slg_decode_params* dp,
+                                          const slg_calib* calib, const slg_tri_params* tp, void* workspace,
+                                          int64_t ws_stride, const slg_cloud* outs, const slg_capture* next,
+                                          int32_t n_next, void* const* timing_events, void* stream) {
+  return fused_batch(caps, n_views, dp, calib, tp, static_cast<char*>(workspace), ws_stride, outs, timing_events,
+                     static_cast<hipStream_t>(stream), next, next ? n_next : 0);
+}
+
+int32_t slg_decode_stats_partials_batch(int32_t n_views, int32_t height, int32_t width, const slg_decode_params* dp,
+                                        void* workspace, int64_t ws_stride, void* stream) {
+  if (n_views < 1 || !dp || !workspace || height < 1 || width < 1) return fail(SLG_ERR_INVALID, "bad argument");
+  if (dp->thresh_mode != SLG_THRESH_OTSU) return fail(SLG_ERR_UNSUPPORTED, "partial histograms are Otsu only");
+  const int64_t n_px = int64_t(height) * width;
+  if (n_views > 1 && (ws_stride < ws_total(n_px) || (ws_stride & 255)))
+    return fail(SLG_ERR_INVALID, "ws_stride too small or not 256-aligned");
+  char* ws = static_cast<char*>(workspace);
+  for (int v0 = 0; v0 < n_views; v0 += kMaxBatch) {
+    const int nb = n_views - v0 < kMaxBatch ? n_views - v0 : kMaxBatch;
+    const int rc = stats_launch_batch(nullptr, nullptr, nb, n_px, dp, ws + int64_t(v0) * ws_stride, ws_stride,
+                                      static_cast<hipStream_t>(stream), true);
+    if (rc) return rc;
+  }
+  return SLG_OK;
 }
 
 int32_t slg_rays_match_pinhole(const double* rays, int32_t height, int32_t width, double fx, double fy, double cx,

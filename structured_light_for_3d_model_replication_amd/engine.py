@@ -374,10 +374,32 @@ class BatchReconstructor:
                                                      self._ws(pb.slot), self.ws_stride, pb.clouds,
                                                      self._events_arg(pb, events), _stream(stream)))
 
-    def run_pipelined(self, batches, main_stream, stats_stream, events=None):
-        """Run ``batches`` (PreparedBatch list; consecutive ones on different slots) with the
-        stats of batch k+1 on ``stats_stream`` overlapping batch k's fused launch on
-        ``main_stream``.  ``events[k]``: timing events for batch k's fused launches, or None."""
+    def main_next(self, pb: PreparedBatch, nxt: PreparedBatch, events=None, stream=None):
+        """Fused launch of ``pb`` that also histograms ``nxt`` (the batch after next, same
+        slot) into the slot's per-tile partials (``slg_decode_triangulate_batch_next``)."""
+        if nxt.slot != pb.slot or nxt.n > pb.n:
+            raise ValueError("the carried batch must use this batch's slot and have no more views")
+        N.check(N.lib().slg_decode_triangulate_batch_next(
+            pb.caps, pb.n, ctypes.byref(pb.dp), ctypes.byref(pb.calib), ctypes.byref(pb.tp), self._ws(pb.slot),
+            self.ws_stride, pb.clouds, nxt.caps, nxt.n, self._events_arg(pb, events), _stream(stream)))
+
+    def stats_partials(self, pb: PreparedBatch, stream=None):
+        """Thresholds of ``pb`` from the partials a fused launch left in its slot."""
+        N.check(N.lib().slg_decode_stats_partials_batch(pb.n, self.height, self.width, ctypes.byref(pb.dp),
+                                                        self._ws(pb.slot), self.ws_stride, _stream(stream)))
+
+    def run_pipelined(self, batches, main_stream, stats_stream, events=None, mode="fused"):
+        """Run ``batches`` (PreparedBatch list; consecutive ones on different slots) with their
+        stats off the fused launches' critical path.
+
+        mode "overlap": the stats pass of batch k+1 runs on ``stats_stream`` beside batch k's
+        fused launch on ``main_stream``.
+        mode "fused": batch k's fused launch also computes batch k+2's Otsu histograms (per-tile
+        partials, no second pass over its white/black frames); a small kernel on
+        ``stats_stream`` turns them into thresholds beside batch k+1's launch.  Needs Otsu
+        thresholds and slots alternating k % 2; the first two batches (and any batch with more
+        views than the one carrying it) get a regular stats pass.
+        ``events[k]``: timing events for batch k's fused launches, or None."""
         n = len(batches)
         for k in range(1, n):
             if batches[k].slot == batches[k - 1].slot:
@@ -385,6 +407,28 @@ class BatchReconstructor:
         while len(self._events) < 2 * n:
             self._events.append(torch.cuda.Event())
         st_ev, mn_ev = self._events[0::2], self._events[1::2]
+        if mode == "fused" and n and all(b.dp.thresh_mode == N.THRESH_OTSU for b in batches):
+            for k in range(min(2, n)):
+                self.stats(batches[k], stream=stats_stream)
+                st_ev[k].record(stats_stream)
+            for k in range(n):
+                nxt = batches[k + 2] if k + 2 < n else None
+                carry = nxt is not None and nxt.slot == batches[k].slot and nxt.n <= batches[k].n
+                main_stream.wait_event(st_ev[k])
+                ev = None if events is None else events[k]
+                if carry:
+                    self.main_next(batches[k], nxt, events=ev, stream=main_stream)
+                else:
+                    self.main(batches[k], events=ev, stream=main_stream)
+                mn_ev[k].record(main_stream)
+                if nxt is not None:                        # batch k+2 reuses batch k's slot
+                    stats_stream.wait_event(mn_ev[k])
+                    (self.stats_partials if carry else self.stats)(nxt, stream=stats_stream)
+                    st_ev[k + 2].record(stats_stream)
+            stats_stream.wait_event(mn_ev[n - 1])
+            return
+        if mode not in ("fused", "overlap"):
+            raise ValueError(f"unknown pipeline mode {mode!r}")
         if n:
             self.stats(batches[0], stream=stats_stream)
             st_ev[0].record(stats_stream)

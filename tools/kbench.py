@@ -91,6 +91,9 @@ def main():
         beng.stats(pb)
         torch.cuda.synchronize()
         run(f"stats_batch{nb}", lambda v: beng.stats(pb))
+        os.environ["SLG_DBG"] = "16"                 # Otsu replaced by a constant
+        run(f"stats_batch{nb}_no_otsu", lambda v: beng.stats(pb))
+        os.environ.pop("SLG_DBG")
         tags = [("", None)]
         if nb == len(dfr):
             tags += [(f"_dbg{d}", str(d)) for d in (1, 2, 4, 7)]
@@ -102,6 +105,16 @@ def main():
             run(name, lambda v: beng.main(pb), pre=lambda v: beng.stats(pb),   # stats re-arm the look-back
                 alg_bytes=nb * (frame_b1 + 18 * pts[1]))
             os.environ.pop("SLG_DBG", None)
+            if name in res:
+                res[name]["per_view_us"] = round(res[name]["median_us"] / nb, 2)
+                print(name, "per view", res[name]["per_view_us"], file=sys.stderr, flush=True)
+        if nb == len(dfr):                           # the same launch carrying a batch's histograms
+            name = f"main3_batch{nb}_next"
+            dfr2 = [E.DeviceFrames(list(v.frames), v.texture) for v in views]   # distinct buffers: cold
+            pbn = beng.prepare(dfr2, cfg, dcal, bclouds, 1)
+            run(name, lambda v: beng.main_next(pb, pbn), pre=lambda v: beng.stats(pb),
+                alg_bytes=nb * (frame_b1 + 18 * pts[1]))
+            run(f"stats_partials{nb}", lambda v: beng.stats_partials(pb))
             if name in res:
                 res[name]["per_view_us"] = round(res[name]["median_us"] / nb, 2)
                 print(name, "per view", res[name]["per_view_us"], file=sys.stderr, flush=True)
@@ -133,28 +146,29 @@ def main():
     bclouds = [[E.Cloud(H * W, 1, False) for _ in range(nb)] for _ in range(2)]
     pbs = [beng.prepare(dfr, cfg, dcal, bclouds[k], 1, slot=k) for k in range(2)]
     s2 = torch.cuda.Stream()
-    for rep in range(2):
-        seq = [pbs[k % 2] for k in range(8)]
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        a.record(s)
-        s2.wait_stream(s)
-        beng.run_pipelined(seq, s, s2)
-        s.wait_stream(s2)
-        b.record(s)
-        torch.cuda.synchronize()
-        us = a.elapsed_time(b) * 1e3 / (8 * nb)
-    res["pipelined_per_view_us"] = round(us, 2)
-    print("pipelined per view", round(us, 2), file=sys.stderr, flush=True)
+    for mode in ("overlap", "fused"):
+        for rep in range(2):
+            seq = [pbs[k % 2] for k in range(16)]
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            a.record(s)
+            s2.wait_stream(s)
+            beng.run_pipelined(seq, s, s2, mode=mode)
+            s.wait_stream(s2)
+            b.record(s)
+            torch.cuda.synchronize()
+            us = a.elapsed_time(b) * 1e3 / (16 * nb)
+        res[f"pipelined_{mode}_per_view_us"] = round(us, 2)
+        print(f"pipelined {mode} per view", round(us, 2), file=sys.stderr, flush=True)
     for rep in range(2):                             # stats + fused launch on one stream
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         a.record(s)
-        for k in range(8):
+        for k in range(16):
             beng.run(pbs[k % 2], stream=s)
         b.record(s)
         torch.cuda.synchronize()
-        us = a.elapsed_time(b) * 1e3 / (8 * nb)
+        us = a.elapsed_time(b) * 1e3 / (16 * nb)
     res["serial_per_view_us"] = round(us, 2)
     print("serial per view", round(us, 2), file=sys.stderr, flush=True)
     run("decode", lambda v: eng.decode(dfr[v], cfg), alg_bytes=(44 + 9) * n_px)
