@@ -71,7 +71,7 @@ def load_traffic_per_view():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--steps", type=int, default=1200)
     ap.add_argument("--warmup", type=int, default=24)
     ap.add_argument("--views", type=int, default=12, help="distinct rendered views")
     ap.add_argument("--copies", type=int, default=3, help="device copies of each view in the pool")

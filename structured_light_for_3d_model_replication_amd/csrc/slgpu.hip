@@ -67,8 +67,9 @@ struct WsHeader {
   double thr_s;            // float thresholds (for inspection / tests)
   double thr_c;
   int64_t totals[2];       // column / row stream point totals
-  uint64_t prof[6];        // SLG_DBG bit 6 (profiling): main3 phase time sums (100 MHz ticks):
-                           // A decode, B triangulate, C look-back, D stores; [4] workgroups
+  uint64_t prof[8];        // SLG_DBG bit 6 (profiling): main3 phase time sums (100 MHz ticks):
+                           // A decode, B triangulate, C look-back, D stores; [4] workgroups;
+                           // look-back [5] state-load rounds, [6] windows, [7] sleep units
 };
 constexpr int kHistCopies = 16;            // partial histograms: blocks spread their atomics
 constexpr int64_t kHistPartOff = 8192;      // uint32 [kHistCopies][2][256] after the header
@@ -812,7 +813,10 @@ __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int ag
   const unsigned help_after = (p.dbg & 32) ? 0u : kHelpAfter;                       // dbg 32: tests
   uint64_t excl = 0;
   int64_t j = tile - 1;
+  unsigned n_rounds = 0, n_windows = 0, n_slept = 0;   // profiling (dbg bit 6)
   for (;;) {
+    ++n_windows;
+    ++n_rounds;
     uint64_t vv[kLookK];
 #pragma unroll
     for (int k = 0; k < kLookK; ++k) {
@@ -839,6 +843,8 @@ __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int ag
       }
       for (unsigned z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(2);
       slept += nap;
+      n_slept += nap;
+      ++n_rounds;
       nap = nap < nap_cap ? nap * 2 : nap_cap;
 #pragma unroll
       for (int k = 0; k < kLookK; ++k) {
@@ -856,6 +862,11 @@ __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int ag
   }
   if (lane == 0) st_state(&st[tile], kFlagInc | (excl + uint64_t(agg)));
   excl_out = excl;
+  if ((p.dbg & 64) && lane == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&p.ws->prof[5]), (unsigned long long)n_rounds);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&p.ws->prof[6]), (unsigned long long)n_windows);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&p.ws->prof[7]), (unsigned long long)n_slept);
+  }
   return true;
 }
 
@@ -905,6 +916,9 @@ __global__ __launch_bounds__(kBlock) void decode_maps_kernel(MainParams p) {
 // 20 KB of LDS and no point staging keep several workgroups per CU resident, so one tile's
 // decode stream overlaps other tiles' fp64 work and look-back.
 constexpr int kMaxViews = 16;
+#ifndef SLG_DECODE_BATCH
+#define SLG_DECODE_BATCH 11                // pairs per axis in flight per lane (4/6/8/11: 31.7/30.3/28.7/27.5 us/view)
+#endif
 #ifndef SLG_VIEW_MAJOR
 #define SLG_VIEW_MAJOR 0                   // 1: all tiles of view 0 first, then view 1, ...
 #endif
@@ -1111,7 +1125,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     }
     uint32_t valid;
     int col[kPx], row[kPx];
-    decode_lane<ROW_MODE, SRC_FRAMES, 8>(p, px0, tail, valid, col, row);
+    decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH>(p, px0, tail, valid, col, row);
     const int2 sc = block_scan(__popc(valid), s_wtot);
     n_items = sc.y;
     int m = sc.x;

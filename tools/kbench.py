@@ -126,7 +126,11 @@ def main():
         pb = beng.prepare(dfr, cfg, dcal, bclouds, 1)
 
         def prof():
-            return np.frombuffer(beng.header(0, 0)[3136:3136 + 48].cpu().numpy().tobytes(), np.uint64).astype(np.float64)
+            h = [np.frombuffer(beng.header(0, v)[3136:3136 + 64].cpu().numpy().tobytes(), np.uint64).astype(np.float64)
+                 for v in range(nb)]
+            out = h[0].copy()                        # phases sum into view 0; look-back counts per view
+            out[5:] = sum(x[5:] for x in h)
+            return out
         os.environ["SLG_DBG"] = "64"
         p0 = prof()
         for _ in range(6):
@@ -138,6 +142,9 @@ def main():
         wgs = max(d[4], 1.0)
         ph = {k: round(d[i] / wgs * 0.01, 3) for i, k in enumerate(["A_decode", "B_tri", "C_lookback", "D_stores"])}
         ph["workgroups"] = int(d[4])
+        ph["polls_per_tile"] = round(d[5] / wgs, 3)
+        ph["windows_per_tile"] = round(d[6] / wgs, 3)
+        ph["sleep_units_per_tile"] = round(d[7] / wgs, 2)
         res["phase_us_per_workgroup"] = ph
         print("phase us per workgroup", ph, file=sys.stderr, flush=True)
     # pipelined: stats of batch k+1 on a side stream during batch k's fused launch
