@@ -67,9 +67,7 @@ struct WsHeader {
   double thr_s;            // float thresholds (for inspection / tests)
   double thr_c;
   int64_t totals[2];       // column / row stream point totals
-  uint64_t prof[8];        // SLG_DBG bit 6 (profiling): main3 phase time sums (100 MHz ticks):
-                           // A decode, B triangulate, C look-back, D stores; [4] workgroups;
-                           // look-back [5] state-load rounds, [6] windows, [7] sleep units
+  uint64_t pad3[8];
 };
 constexpr int kHistCopies = 16;            // partial histograms: blocks spread their atomics
 constexpr int64_t kHistPartOff = 8192;      // uint32 [kHistCopies][2][256] after the header
@@ -94,6 +92,20 @@ __device__ inline uint64_t ld_state(const uint64_t* p) {
 }
 __device__ inline void st_state(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+#ifndef SLG_NT_LOADS
+#define SLG_NT_LOADS 1                     // frames / texture are read once: non-temporal loads
+#endif
+// Once-read stream (frames, texture): non-temporal 8-byte load (global_load_dwordx2 nt).
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ inline uint2 ld_once8(const void* ptr) {
+#if SLG_NT_LOADS
+  const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(ptr));
+  return make_uint2(v.x, v.y);
+#else
+  return *reinterpret_cast<const uint2*>(ptr);
+#endif
 }
 
 template <class T>
@@ -344,8 +356,8 @@ __device__ inline void hist_load(const uint8_t* white, const uint8_t* black, int
   for (int h = 0; h < 2; ++h) {             // two 8-byte loads
     const int64_t o = c + 16 * lane + 8 * h;
     const int64_t so = o < n_px ? o : 0;    // frames readable to round_up(n, 8)
-    uint2 wq = *reinterpret_cast<const uint2*>(white + so);
-    uint2 bq = *reinterpret_cast<const uint2*>(black + so);
+    uint2 wq = ld_once8(white + so);
+    uint2 bq = ld_once8(black + so);
     if (o + 8 > n_px) {                     // tail: zero the bytes at or past n_px
       const int64_t keep = n_px - o;        // <= 0: none
       const uint64_t mk = keep <= 0 ? 0 : (~0ull >> (64 - 8 * keep));
@@ -547,7 +559,7 @@ struct MainParams {
   double fx, fy, cx, cy;
   double rfx, rfy;            // RN(1/fx), RN(1/fy) when div_fast (Markstein divisions)
   int32_t div_fast;
-  int32_t pad1;
+  int32_t rays_fast;          // host-verified: every pixel's ray takes the Markstein path (tri_item FAST)
   double o0, o1, o2;
   const double* pcol;
   int32_t n_pcol;
@@ -586,7 +598,7 @@ __device__ inline void acc_pair(uint32_t (&acc)[4], uint2 pv, uint2 iv) {
 
 // 8 frame bytes at pixel lp (clamped in-bounds by the caller; rows are padded to >= 8 px).
 __device__ inline uint2 ld_frame8(const MainParams& p, int frame, int64_t lp) {
-  return *reinterpret_cast<const uint2*>(p.frames + int64_t(frame) * p.stride + lp);
+  return ld_once8(p.frames + int64_t(frame) * p.stride + lp);
 }
 
 // Decode the 8 pixels of one lane: mask bits + column / row codes.  Frame loads of both axes
@@ -687,7 +699,10 @@ struct TriOut {
 };
 
 // Ray-plane intersection of one valid pixel (processing.py:143-234), fp64 in NumPy's order.
-template <int ROW_MODE, int RAYS>
+// FAST (p.rays_fast, checked on the host for every column and row of the image): the
+// Markstein conditions hold for every pixel, so the code is one straight-line block with no
+// per-lane fallback branches -- the same values, and two items per lane interleave (phase B).
+template <int ROW_MODE, int RAYS, bool FAST = false>
 __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int v) {
   const double2* qc = reinterpret_cast<const double2*>(p.pcol + 4 * int64_t(code & 0xffffu));
   const double2 pc01 = qc[0], pc23 = qc[1];
@@ -702,11 +717,17 @@ __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int
     // The same IEEE quotients as the reference, with the divisions by fx, fy (per camera)
     // and by the norm (three per pixel) done as Markstein corrections of one reciprocal.
     const double ax = double(u) - p.cx, ay = double(v) - p.cy;
-    const double x = p.div_fast && div_rn_ok(ax) ? div_rn(ax, p.fx, p.rfx) : ax / p.fx;   // processing.py:150
-    const double y = p.div_fast && div_rn_ok(ay) ? div_rn(ay, p.fy, p.rfy) : ay / p.fy;   // processing.py:151
+    double x, y;
+    if constexpr (FAST) {
+      x = div_rn(ax, p.fx, p.rfx);                         // processing.py:150
+      y = div_rn(ay, p.fy, p.rfy);                         // processing.py:151
+    } else {
+      x = p.div_fast && div_rn_ok(ax) ? div_rn(ax, p.fx, p.rfx) : ax / p.fx;
+      y = p.div_fast && div_rn_ok(ay) ? div_rn(ay, p.fy, p.rfy) : ay / p.fy;
+    }
     const double n = sqrt((x * x + y * y) + 1.0);          // np.linalg.norm(rays, axis=0)
     r2 = 1.0 / n;                                          // rays /= norms
-    if (n < 0x1p900 && div_rn_ok(x) && div_rn_ok(y)) {     // n >= 1: its reciprocal is normal
+    if (FAST || (n < 0x1p900 && div_rn_ok(x) && div_rn_ok(y))) {   // n >= 1: its reciprocal is normal
       r0 = div_rn(x, n, r2); r1 = div_rn(y, n, r2);
     } else {
       r0 = x / n; r1 = y / n;
@@ -719,7 +740,13 @@ __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int
   const double den = (pc01.x * r0 + pc01.y * r1) + pc23.x * r2;          // np.sum(N*rays, 0)
   const double num = ((pc01.x * p.o0 + pc01.y * p.o1) + pc23.x * p.o2) + pc23.y;
   const bool okc = fabs(den) > 1e-6;
-  const double t = okc ? (-num) / den : 0.0;
+  double t;
+  if constexpr (FAST) {
+    const double q = (-num) / den;                         // unconditional: a select, not a branch
+    t = okc ? q : 0.0;
+  } else {
+    t = okc ? (-num) / den : 0.0;
+  }
   o.x = p.o0 + r0 * t; o.y = p.o1 + r1 * t; o.z = p.o2 + r2 * t;
   o.keep = okc;
   o.rx = o.ry = o.rz = 0.0;
@@ -731,7 +758,13 @@ __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int
     const double dr = (pr01.x * r0 + pr01.y * r1) + pr23.x * r2;
     const double nr = ((pr01.x * p.o0 + pr01.y * p.o1) + pr23.x * p.o2) + pr23.y;
     const bool okr = fabs(dr) > 1e-6;
-    const double tr = okr ? (-nr) / dr : 0.0;
+    double tr;
+    if constexpr (FAST) {
+      const double q = (-nr) / dr;
+      tr = okr ? q : 0.0;
+    } else {
+      tr = okr ? (-nr) / dr : 0.0;
+    }
     o.rx = p.o0 + r0 * tr; o.ry = p.o1 + r1 * tr; o.rz = p.o2 + r2 * tr;
     o.keep |= uint32_t(okr) << 1;
   }
@@ -800,7 +833,7 @@ constexpr unsigned kHelpAfter = 2048;   // s_sleep(2) units (~0.1 ms) before ask
 // (tile_keep_count_wave) and retries, so waiting always ends.  Re-polls only the entries
 // newer than the nearest inclusive prefix, with capped back-off.
 __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int agg, uint64_t& excl_out,
-                             int& help_tile) {
+                             int& help_tile, uint32_t& polls, uint32_t& naps) {
   const int lane = threadIdx.x & 63;
   if (p.dbg & 1) { excl_out = uint64_t(tile) * kTilePx; return true; }   // ablation: no wait
   if (tile == 0) {
@@ -813,10 +846,8 @@ __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int ag
   const unsigned help_after = (p.dbg & 32) ? 0u : kHelpAfter;                       // dbg 32: tests
   uint64_t excl = 0;
   int64_t j = tile - 1;
-  unsigned n_rounds = 0, n_windows = 0, n_slept = 0;   // profiling (dbg bit 6)
   for (;;) {
-    ++n_windows;
-    ++n_rounds;
+    ++polls;
     uint64_t vv[kLookK];
 #pragma unroll
     for (int k = 0; k < kLookK; ++k) {
@@ -843,8 +874,8 @@ __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int ag
       }
       for (unsigned z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(2);
       slept += nap;
-      n_slept += nap;
-      ++n_rounds;
+      naps += nap;
+      ++polls;
       nap = nap < nap_cap ? nap * 2 : nap_cap;
 #pragma unroll
       for (int k = 0; k < kLookK; ++k) {
@@ -862,11 +893,6 @@ __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int ag
   }
   if (lane == 0) st_state(&st[tile], kFlagInc | (excl + uint64_t(agg)));
   excl_out = excl;
-  if ((p.dbg & 64) && lane == 0) {
-    atomicAdd(reinterpret_cast<unsigned long long*>(&p.ws->prof[5]), (unsigned long long)n_rounds);
-    atomicAdd(reinterpret_cast<unsigned long long*>(&p.ws->prof[6]), (unsigned long long)n_windows);
-    atomicAdd(reinterpret_cast<unsigned long long*>(&p.ws->prof[7]), (unsigned long long)n_slept);
-  }
   return true;
 }
 
@@ -990,8 +1016,8 @@ __device__ inline void hist_next_load(const uint8_t* white, const uint8_t* black
   wq = make_uint2(0, 0);
   bq = make_uint2(0, 0);
   if (o < n_px) {                            // frames readable to round_up(n, 8)
-    wq = *reinterpret_cast<const uint2*>(white + o);
-    bq = *reinterpret_cast<const uint2*>(black + o);
+    wq = ld_once8(white + o);
+    bq = ld_once8(black + o);
   }
 }
 
@@ -1094,12 +1120,16 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   const int64_t px0 = tile_px + int64_t(tid) * kPx;
   const bool tail = tile == tiles - 1;               // block-uniform: guarded reads only here
   const int tile_v0 = int(tile_px / p.width);
-  const bool prof = (p.dbg & 64) != 0;               // phase timing (profiling builds of a run)
+  // Profiling (SLG_DBG bit 6): per workgroup one 32-byte record {A decode, B triangulate,
+  // C look-back, D stores (100 MHz ticks), look-back polls, sleep units, items, start} written
+  // to view 0's partials region (tools/kbench.py "phases"; unused unless batches are carried).
+  const bool prof = (p.dbg & 64) != 0;
   uint64_t t_phase = prof ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint32_t rec[8] = {0, 0, 0, 0, 0, 0, 0, uint32_t(t_phase)};   // [7]: start time (low 32 bits)
   auto stamp = [&](int k) {
     if (prof && tid == 0) {
       const uint64_t t = __builtin_amdgcn_s_memrealtime();
-      atomicAdd(reinterpret_cast<unsigned long long*>(&P.v[0].ws->prof[k]), (unsigned long long)(t - t_phase));
+      rec[k] = uint32_t(t - t_phase);
       t_phase = t;
     }
   };
@@ -1116,8 +1146,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   {
     uint32_t tex[6] = {0, 0, 0, 0, 0, 0};
     if (!tail) {
-      const uint2* tq = reinterpret_cast<const uint2*>(p.texture + px0 * 3);
-      const uint2 t0 = tq[0], t1 = tq[1], t2 = tq[2];
+      const uint8_t* tq = p.texture + px0 * 3;
+      const uint2 t0 = ld_once8(tq), t1 = ld_once8(tq + 8), t2 = ld_once8(tq + 16);
       tex[0] = t0.x; tex[1] = t0.y; tex[2] = t1.x; tex[3] = t1.y; tex[4] = t2.x; tex[5] = t2.y;
     } else {
       for (int k = 0; k < 3 * kPx; ++k)
@@ -1151,6 +1181,42 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // ~15 VGPRs for a fifth wave per SIMD but measured 6% slower).
   XT pts[NS][kIt][3];
   uint64_t km[NS][kIt];
+  static_assert(kIt % 2 == 0, "paired rounds");
+  if (p.rays_fast && !(p.dbg & 2)) {
+    // Two rounds per step: two independent straight-line fp64 chains (and their plane
+    // gathers) per lane, so the latency of one hides behind the other.
+#pragma unroll
+    for (int i = 0; i < kIt; i += 2) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) km[s][i] = km[s][i + 1] = 0;
+      if (i * kB < n_items) {                        // block-uniform
+        TriOut o[2];
+        bool in[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int m = tid + kB * (i + h);
+          in[h] = m < n_items;
+          const uint32_t sc = s_code[m], suv = s_uv[m];   // m < kTilePx; garbage past n_items masked
+          const uint32_t code = in[h] ? sc : 0u, uv = in[h] ? suv : 0u;
+          o[h] = tri_item<ROW_MODE, RAYS, true>(p, code, int(uv & 0xffffu), int(uv >> 16));
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t keep = in[h] ? o[h].keep : 0u;
+          pts[0][i + h][0] = XT(o[h].x); pts[0][i + h][1] = XT(o[h].y); pts[0][i + h][2] = XT(o[h].z);
+          if constexpr (ROW_MODE == 2) {
+            pts[NS - 1][i + h][0] = XT(o[h].rx); pts[NS - 1][i + h][1] = XT(o[h].ry); pts[NS - 1][i + h][2] = XT(o[h].rz);
+          }
+#pragma unroll
+          for (int s = 0; s < NS; ++s) km[s][i + h] = __ballot((keep >> s) & 1u);
+        }
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) { s_cnt[s][i][wave] = __popcll(km[s][i]); s_cnt[s][i + 1][wave] = __popcll(km[s][i + 1]); }
+      }
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < kIt; ++i) {
 #pragma unroll
@@ -1180,6 +1246,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       for (int s = 0; s < NS; ++s) s_cnt[s][i][wave] = __popcll(km[s][i]);
     }
   }
+  }
   if (hn) hist_next_stage(hn_w, hn_b, p.n_px, px0, s_hstage);
   __syncthreads();
 
@@ -1193,7 +1260,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       uint64_t* st = p.states + int64_t(s) * tiles;
       uint64_t excl;
       int ht;
-      while (!lookback_try(p, st, tile, agg, excl, ht)) {
+      while (!lookback_try(p, st, tile, agg, excl, ht, rec[4], rec[5])) {
         // a predecessor has not published for long (it may not be dispatched yet): publish
         // its aggregate for it, computed by this wave, and look back again
         const int hagg = tile_keep_count_wave<ROW_MODE, SRC_FRAMES, RAYS>(p, ht, s);
@@ -1246,7 +1313,12 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   if (prof) {
     __syncthreads();
     stamp(3);
-    if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&P.v[0].ws->prof[4]), 1ull);
+    if (tid == 0) {
+      rec[6] = uint32_t(n_items);
+      uint4* out = reinterpret_cast<uint4*>(reinterpret_cast<char*>(P.v[0].ws) + parts_off(p.n_px)) + 2 * blockIdx.x;
+      out[0] = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+      out[1] = make_uint4(rec[4], rec[5], rec[6], rec[7]);
+    }
   }
 }
 
@@ -1429,6 +1501,20 @@ int fill_calib(MainParams& mp, const slg_calib* c, const slg_tri_params* tp, int
   mp.rfx = 1.0 / c->fx;
   mp.rfy = 1.0 / c->fy;
   mp.div_fast = vetted(c->fx) && vetted(c->fy) ? 1 : 0;
+  // rays_fast: tri_item's Markstein conditions hold for every column and row of the image
+  // (x = (u-cx)/fx and y = (v-cy)/fy in range, so n = |(x, y, 1)| < 2^450 as well).
+  auto ok_num = [](double a) { const double m = fabs(a); return m == 0.0 || (m > 0x1p-900 && m < 0x1p900); };
+  bool fast = c->ray_mode == SLG_RAYS_TABLE || mp.div_fast;
+  const int64_t height = width > 0 ? n_px / width : 0;
+  for (int64_t u = 0; fast && c->ray_mode == SLG_RAYS_PINHOLE && u < width; ++u) {
+    const double ax = double(u) - c->cx, x = ax / c->fx;
+    fast = ok_num(ax) && ok_num(x) && fabs(x) < 0x1p449;
+  }
+  for (int64_t v = 0; fast && c->ray_mode == SLG_RAYS_PINHOLE && v < height; ++v) {
+    const double ay = double(v) - c->cy, y = ay / c->fy;
+    fast = ok_num(ay) && ok_num(y) && fabs(y) < 0x1p449;
+  }
+  mp.rays_fast = fast ? 1 : 0;
   mp.o0 = c->oc[0]; mp.o1 = c->oc[1]; mp.o2 = c->oc[2];
   mp.pcol = c->col_planes; mp.n_pcol = c->n_col_planes;
   mp.prow = c->row_planes; mp.n_prow = c->n_row_planes;

@@ -118,35 +118,67 @@ def main():
             if name in res:
                 res[name]["per_view_us"] = round(res[name]["median_us"] / nb, 2)
                 print(name, "per view", res[name]["per_view_us"], file=sys.stderr, flush=True)
-    # phase timing of the fused kernel (SLG_DBG bit 6: per-workgroup s_memrealtime stamps)
+    # phase timing of the fused kernel (SLG_DBG bit 6: one 32-byte record per workgroup in view
+    # 0's partials region: A, B, C, D in 100 MHz ticks, polls, sleep units, items, view)
     if not want or "phases" in want:
         nb = len(dfr)
         beng = E.BatchReconstructor(H, W, nb)
         bclouds = [E.Cloud(H * W, 1, False) for _ in range(nb)]
         pb = beng.prepare(dfr, cfg, dcal, bclouds, 1)
-
-        def prof():
-            h = [np.frombuffer(beng.header(0, v)[3136:3136 + 64].cpu().numpy().tobytes(), np.uint64).astype(np.float64)
-                 for v in range(nb)]
-            out = h[0].copy()                        # phases sum into view 0; look-back counts per view
-            out[5:] = sum(x[5:] for x in h)
-            return out
-        os.environ["SLG_DBG"] = "64"
-        p0 = prof()
-        for _ in range(6):
-            beng.stats(pb)
-            beng.main(pb)
-        torch.cuda.synchronize()
-        d = prof() - p0
-        os.environ.pop("SLG_DBG")
-        wgs = max(d[4], 1.0)
-        ph = {k: round(d[i] / wgs * 0.01, 3) for i, k in enumerate(["A_decode", "B_tri", "C_lookback", "D_stores"])}
-        ph["workgroups"] = int(d[4])
-        ph["polls_per_tile"] = round(d[5] / wgs, 3)
-        ph["windows_per_tile"] = round(d[6] / wgs, 3)
-        ph["sleep_units_per_tile"] = round(d[7] / wgs, 2)
-        res["phase_us_per_workgroup"] = ph
-        print("phase us per workgroup", ph, file=sys.stderr, flush=True)
+        al = lambda x: (x + 255) // 256 * 256
+        n_tiles = (n_px + 2047) // 2048
+        parts_off = 65536 + al(2 * n_tiles * 8) + al(n_px * 24) + al(n_px * 3)
+        n_wg = n_tiles * nb
+        for extra in (0, 1, 2):                      # + ablations: no wait / trivial tri
+            os.environ["SLG_DBG"] = str(64 | extra)
+            recs, us = [], 0.0
+            for _ in range(4):
+                beng.stats(pb)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                beng.main(pb)
+                b.record(s)
+                torch.cuda.synchronize()
+                us += a.elapsed_time(b) * 1e3
+                raw = beng.workspace[parts_off: parts_off + n_wg * 32].cpu().numpy()
+                recs.append(np.frombuffer(raw.tobytes(), np.uint32).reshape(n_wg, 8).astype(np.float64))
+            os.environ.pop("SLG_DBG")
+            r = np.concatenate(recs)
+            ph = {k: round(float(r[:, i].mean()) * 0.01, 3) for i, k in enumerate(["A_decode", "B_tri", "C_lookback", "D_stores"])}
+            ph["lifetime"] = round(float(r[:, :4].sum(1).mean()) * 0.01, 2)
+            ph["polls_per_tile"] = round(float(r[:, 4].mean()), 2)
+            ph["sleep_units_per_tile"] = round(float(r[:, 5].mean()), 1)
+            ph["items_per_tile"] = round(float(r[:, 6].mean()), 1)
+            ph["C_p50_p90_p99"] = [round(float(np.percentile(r[:, 2], q)) * 0.01, 2) for q in (50, 90, 99)]
+            # look-back wait vs this tile's items and its predecessor's (same view): content skew
+            rr = recs[-1]
+            tile_of = np.arange(n_wg) // nb
+            pred = np.where(tile_of > 0, np.arange(n_wg) - nb, -1)
+            mine, theirs = rr[:, 6], np.where(pred >= 0, rr[np.maximum(pred, 0), 6], 0)
+            for lbl, sel in (("C_when_pred_heavier", theirs > mine + 256), ("C_when_pred_lighter", theirs + 256 < mine),
+                             ("C_when_similar", np.abs(theirs - mine) <= 256)):
+                ph[lbl] = round(float(rr[sel, 2].mean()) * 0.01, 2) if sel.any() else None
+            # phase occupancy over time (last run): mean / p10 / p90 of workgroups in A and B+C+D
+            t0 = rr[:, 7] - rr[:, 7].min()
+            ends = np.cumsum(rr[:, :4], axis=1)
+            grid = np.arange(0, float((t0 + ends[:, 3]).max()), 10.0)   # 0.1 us steps
+            inA = np.zeros_like(grid)
+            inR = np.zeros_like(grid)
+            for st, e in zip(t0, ends):
+                a0, a1 = np.searchsorted(grid, [st, st + e[0]])
+                inA[a0:a1] += 1
+                r0_, r1_ = np.searchsorted(grid, [st + e[0], st + e[3]])
+                inR[r0_:r1_] += 1
+            mid = slice(len(grid) // 10, len(grid) * 9 // 10)
+            ph["in_A_mean_p10_p90"] = [round(float(inA[mid].mean()), 1), round(float(np.percentile(inA[mid], 10)), 1),
+                                       round(float(np.percentile(inA[mid], 90)), 1)]
+            ph["in_BCD_mean"] = round(float(inR[mid].mean()), 1)
+            if extra == 0:
+                np.save(os.path.join(ROOT, "gpurun_out", "phase_occupancy.npy"), np.stack([grid, inA, inR]))
+            ph["kernel_us_per_view"] = round(us / 4 / nb, 2)
+            ph["lifetime_sum_over_kernel_x1024"] = round(float(r[:, :4].sum()) * 0.01 / (us * 1024), 3)
+            res[f"phases_dbg{extra}"] = ph
+            print(f"phases (dbg {extra})", ph, file=sys.stderr, flush=True)
     # pipelined: stats of batch k+1 on a side stream during batch k's fused launch
     nb = len(dfr)
     beng = E.BatchReconstructor(H, W, nb, slots=2)
