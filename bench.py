@@ -36,14 +36,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(views, cal, seconds):
+# Workloads (BASELINE.json configs / SURVEY §8(d)).  c2 is the metric's configuration and the
+# default; c4 / c5 are the larger single-view geometries, run on request (--config).
+CONFIGS = {
+    "c2": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 10), n_present=44, views=12, copies=3, batch=12,
+               text="C2: 1920x1080 view, 11 col + 10 row Gray bits + inverses + white/black (44 frames)"),
+    "c4": dict(cam=(6000, 4000), proj=(3840, 2160), nsets=(12, 12), n_present=None, views=2, copies=2, batch=2,
+               text="C4: 6000x4000 view, projector 3840x2160, 12 col + 12 row Gray bits + inverses + "
+                    "white/black (50 frames)"),
+    "c5": dict(cam=(3840, 2160), proj=(1920, 1080), nsets=(11, 11), n_present=None, views=4, copies=2, batch=4,
+               text="C5: 3840x2160 view, projector 1920x1080, 11 col + 11 row Gray bits + inverses + "
+                    "white/black (46 frames)"),
+}
+
+
+def cpu_baseline(views, cal, seconds, wl):
     """Oracle (NumPy port of the reference path) on this host, one thread, frames in memory."""
     import numpy as np
     from oracle import sl_oracle as O
+    (PW, PH), (nc, nr) = wl["proj"], wl["nsets"]
     done, pts, t0 = 0, 0, time.perf_counter()
     while True:
         v = views[done % len(views)]
-        col, row, mask = O.decode_processing(list(v.frames), n_sets_col=11, n_sets_row=10)
+        col, row, mask = O.decode_processing(list(v.frames), n_cols=PW, n_rows=PH, n_sets_col=nc, n_sets_row=nr)
         P, _ = O.reconstruct_processing(col, row, mask, v.texture, cal, row_mode=1)
         pts += len(P)
         done += 1
@@ -51,7 +66,8 @@ def cpu_baseline(views, cal, seconds):
             break
     dt = time.perf_counter() - t0
     return {"value": round(pts / dt / 1e6, 4), "unit": "Mpoints/s", "cores": 1, "kind": "port",
-            "sample": f"{done} C2 views (1920x1080, 11+10 bits, Otsu, row_mode 1), frames in "
+            "sample": f"{done} {wl['text'].split(':')[0]} views ({wl['cam'][0]}x{wl['cam'][1]}, "
+                      f"{nc}+{nr} bits, Otsu, row_mode 1), frames in "
                       f"memory, oracle/sl_oracle.py NumPy restatement, 1 thread, {dt:.1f} s"}
 
 
@@ -73,9 +89,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1200)
     ap.add_argument("--warmup", type=int, default=24)
-    ap.add_argument("--views", type=int, default=12, help="distinct rendered views")
-    ap.add_argument("--copies", type=int, default=3, help="device copies of each view in the pool")
-    ap.add_argument("--batch", type=int, default=12, help="views per fused launch (<= 16)")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
+                    help="workload (default c2, the metric's configuration)")
+    ap.add_argument("--views", type=int, default=None, help="distinct rendered views")
+    ap.add_argument("--copies", type=int, default=None, help="device copies of each view in the pool")
+    ap.add_argument("--batch", type=int, default=None, help="views per fused launch (<= 16)")
     ap.add_argument("--xyz", choices=["f32", "f64"], default="f32")
     ap.add_argument("--pipeline", choices=["serial", "overlap", "fused"], default="fused",
                     help="serial: stats + fused launch per batch on one stream; overlap: the next "
@@ -84,6 +102,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    wl = CONFIGS[args.config]
+    for k in ("views", "copies", "batch"):
+        if getattr(args, k) is None:
+            setattr(args, k, wl[k])
 
     import numpy as np
     import torch
@@ -99,15 +121,15 @@ def main():
 
     from structured_light_for_3d_model_replication_amd import engine as E, synth, _native
 
-    W, H, PW, PH = 1920, 1080, 1920, 1080
+    (W, H), (PW, PH), (NC, NR) = wl["cam"], wl["proj"], wl["nsets"]
     rig = synth.default_rig(W, H, PW, PH)
     cal = rig.tables()
     t = time.perf_counter()
     views = [synth.render_view(rig, view_deg=(rank * args.views + i) * 360.0 / (world * args.views),
-                               seed=1000 * rank + i, n_present=44) for i in range(args.views)]
+                               seed=1000 * rank + i, n_present=wl["n_present"]) for i in range(args.views)]
     log(f"[rank {rank}] rendered {len(views)} views in {time.perf_counter() - t:.1f}s")
 
-    cfg = E.DecodeConfig(PW, PH, 11, 10, "otsu")
+    cfg = E.DecodeConfig(PW, PH, NC, NR, "otsu")
     row_mode, tol, f64 = 1, 2.0, args.xyz == "f64"
     # Device pool: every rendered view uploaded `copies` times (distinct HBM buffers), so a batch
     # never shares frames with the batch before or after next -- e.g. the histograms a fused
@@ -156,7 +178,7 @@ def main():
         b.record(s_main)
     torch.cuda.synchronize()
     out_b = 30 if f64 else 18            # 3 B texture read + 12|24 B XYZ + 3 B BGR per point
-    frame_b = (2 + 2 * (11 + 10)) * H * W
+    frame_b = (2 + 2 * (NC + NR)) * H * W
     total_pts, bytes_alg = 0, 0.0
     for v in range(Wm, Wm + K):
         total_pts += pts[v % P]
@@ -205,14 +227,16 @@ def main():
         achieved = bytes_sum / launches / kern_avg_s / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": (round(load_traffic_per_view() * K / n_launch) if load_traffic_per_view() else None),
+                # committed PMC bytes are per C2 view: other workloads report none
+                "traffic": (round(load_traffic_per_view() * K / n_launch)
+                            if load_traffic_per_view() and args.config == "c2" else None),
                 "kernel": "main3_kernel<1,0,1,1> (fused decode+triangulate+compaction, "
                           f"{B} views per launch)",
                 "kernel_avg_us": round(kern_avg_s * 1e6, 2),
                 "alg_bytes_per_launch": round(bytes_sum / launches)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(views, cal, args.cpu_seconds)
+            cpu = cpu_baseline(views, cal, args.cpu_seconds, wl)
         out = {
             "metric": METRIC,
             "value": round(all_pts / dt_max / 1e6, 2),
@@ -226,9 +250,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": "C2: 1920x1080 view, 11 col + 10 row Gray bits + inverses + "
-                                   "white/black (44 frames), Otsu, row_mode 1 tol 2.0, XYZ "
-                                   f"{args.xyz} + BGR out",
+            "config": {"workload": f"{wl['text']}, Otsu, row_mode 1 tol 2.0, XYZ {args.xyz} + BGR out",
                        "views_per_rank": len(views), "device_pool": P, "points_per_view": int(np.mean(pts)),
                        "batch_views": B,
                        "launches": n_launch,
