@@ -38,6 +38,8 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--kernel", default="main3_kernel")
     ap.add_argument("--tiles-per-view", type=int, default=1013, help="ceil(1920*1080 / 2048)")
+    ap.add_argument("--no-refresh", action="store_true",
+                    help="leave profiles/pmc_main_kernel.json (bench.py's C2 traffic) untouched")
     a = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", a.tag)
     dst = os.path.join(ROOT, "profiles", a.tag)
@@ -75,7 +77,7 @@ def main():
         out["hbm_bytes_per_view"] = round(sum(per.values()))
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
-    if per:
+    if per and not a.no_refresh:
         with open(os.path.join(ROOT, "profiles", "pmc_main_kernel.json"), "w") as f:
             json.dump({"tag": a.tag, "kernel": a.kernel, "hbm_bytes_per_view": out["hbm_bytes_per_view"],
                        "fetch_bytes_per_view": out.get("fetch_size_bytes_per_view"),
