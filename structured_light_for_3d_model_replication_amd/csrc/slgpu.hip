@@ -948,6 +948,9 @@ constexpr int kMaxViews = 16;
 #ifndef SLG_VIEW_MAJOR
 #define SLG_VIEW_MAJOR 0                   // 1: all tiles of view 0 first, then view 1, ...
 #endif
+#ifndef SLG_STAGED_STORES
+#define SLG_STAGED_STORES 0                // 1: phase D via LDS-packed contiguous stores (measured 355 vs 347 us per launch)
+#endif
 #ifndef SLG_M3_WAVES
 #define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
 #endif
@@ -1287,6 +1290,49 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // ------------------------------------------------------------ D: ordered stores from registers
   if (p.dbg & 4) return;                             // ablation: no output stores
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#if SLG_STAGED_STORES
+  // Per wave and round, the kept points are packed in LDS (s_code / s_uv are dead after phase
+  // B) and written back as contiguous elements: each store instruction covers 256 B (f32) of
+  // one run of the cloud instead of a 12-byte-strided scatter, and the BGR bytes likewise.
+  static_assert(4 * 64 * 3 * sizeof(XT) <= sizeof(s_code) && 4 * 64 * 3 <= sizeof(s_uv), "staging");
+  XT* stg = reinterpret_cast<XT*>(s_code) + wave * (64 * 3);
+  uint8_t* stb = reinterpret_cast<uint8_t*>(s_uv) + wave * (64 * 3);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int64_t base = int64_t(s_excl[s]);
+    XT* gx = reinterpret_cast<XT*>(s == 0 ? p.xyz : p.scratch_xyz);
+    uint8_t* gb = s == 0 ? p.bgr : p.scratch_bgr;
+#pragma unroll
+    for (int i = 0; i < kIt; ++i) {
+      int before = 0, round = 0;
+#pragma unroll
+      for (int w = 0; w < kB / 64; ++w) {
+        const int c = s_cnt[s][i][w];
+        before += w < wave ? c : 0;
+        round += c;
+      }
+      const int n3 = 3 * __popcll(km[s][i]);        // wave-uniform
+      if (n3) {
+        if ((km[s][i] >> lane) & 1ull) {
+          const int r = 3 * __popcll(km[s][i] & lt);
+          stg[r] = pts[s][i][0]; stg[r + 1] = pts[s][i][1]; stg[r + 2] = pts[s][i][2];
+          const uint32_t c = s_bgr[tid + kB * i];
+          stb[r] = uint8_t(c); stb[r + 1] = uint8_t(c >> 8); stb[r + 2] = uint8_t(c >> 16);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int64_t q3 = 3 * (base + before);
+        for (int j = lane; j < n3; j += 64) gx[q3 + j] = stg[j];
+        for (int j = lane; j < n3; j += 64) gb[q3 + j] = stb[j];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // reads done before the next round's writes
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      base += round;
+    }
+  }
+#else
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     int64_t base = int64_t(s_excl[s]);
@@ -1310,6 +1356,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       base += round;
     }
   }
+#endif
   if (prof) {
     __syncthreads();
     stamp(3);
