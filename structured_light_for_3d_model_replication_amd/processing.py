@@ -55,8 +55,9 @@ def _needed_frames(n_files, cfg: E.DecodeConfig):
     return need
 
 
-def load_capture(source, cfg: E.DecodeConfig, order=("bmp", "png")):
-    """Discover, decode (host thread pool) and upload one capture: ``(DeviceFrames, texture)``."""
+def read_capture(source, cfg: E.DecodeConfig, order=("bmp", "png")):
+    """Discover and decode (host thread pool) one capture: ``(frame stack, texture)``; frames
+    the decode does not read stay ``None``.  Host work only (safe on a prefetch thread)."""
     files = FR.discover(source, order)
     if len(files) < 4:
         raise ValueError(f"Not enough images (got {len(files)}, need at least 4).")
@@ -66,6 +67,13 @@ def load_capture(source, cfg: E.DecodeConfig, order=("bmp", "png")):
     for i, im in zip(need, imgs):
         stack[i] = im
     texture = FR.imread_bgr(files[0])
+    return stack, texture
+
+
+def load_capture(source, cfg: E.DecodeConfig, order=("bmp", "png"), host=None):
+    """Discover, decode and upload one capture: ``(DeviceFrames, texture)``.  ``host``: the
+    result of :func:`read_capture` when it was already done (e.g. prefetched)."""
+    stack, texture = host if host is not None else read_capture(source, cfg, order)
     return E.DeviceFrames(stack, texture), texture
 
 
@@ -155,10 +163,10 @@ class ProcessingLogic:
         cfg = E.DecodeConfig(1920, 1080, n_sets_col, n_sets_row, thresh_mode, shadow_val,
                              contrast_val, "processing")
 
-        def _process_source(source, out_path, label):
+        def _process_source(source, out_path, label, host=None):
             log(f"  -> Decoding {label}  "
                 f"[col-sets={n_sets_col}  row-sets={n_sets_row}]...")
-            dev, _ = load_capture(source, cfg)
+            dev, _ = load_capture(source, cfg, host=None if host is None else host.result())
             log("  -> Reconstructing 3D points...")
             points, colors = reconstruct_view(dev, cfg, calib_data, row_mode, epipolar_tol)
             log(f"  -> Saving {len(points)} points...")
@@ -183,21 +191,37 @@ class ProcessingLogic:
             subfolders = [f.path for f in os.scandir(target_path) if f.is_dir()]
             log(f"Found {len(subfolders)} subfolders to process.")
 
+            # The next view folder's frames are read and decoded on a prefetch thread while
+            # this one is reconstructed and its PLY written; a read error surfaces (and is
+            # reported) at that folder's turn, as in the reference's per-folder try/except.
+            from concurrent.futures import ThreadPoolExecutor
+            with_imgs = [f for f in subfolders
+                         if glob.glob(os.path.join(f, "*.bmp")) or glob.glob(os.path.join(f, "*.png"))]
             success_count = 0
-            for folder in subfolders:
-                has_imgs = (glob.glob(os.path.join(folder, "*.bmp")) or
-                            glob.glob(os.path.join(folder, "*.png")))
-                if has_imgs:
-                    try:
-                        ply_name = os.path.basename(folder) + ".ply"
-                        out_path = os.path.join(folder, ply_name)
-                        _process_source(folder, out_path,
-                                        f"folder '{os.path.basename(folder)}'")
-                        success_count += 1
-                    except Exception as e:
-                        log(f"  ❌ Error in {os.path.basename(folder)}: {e}\n")
-                else:
-                    log(f"  Skipping {os.path.basename(folder)} (No images found).")
+            with ThreadPoolExecutor(max_workers=1) as pre:
+                pending = {}
+
+                def prefetch(i):
+                    if i < len(with_imgs) and with_imgs[i] not in pending:
+                        pending[with_imgs[i]] = pre.submit(read_capture, with_imgs[i], cfg)
+
+                prefetch(0)
+                k = 0
+                for folder in subfolders:
+                    if k < len(with_imgs) and with_imgs[k] == folder:
+                        k += 1
+                        prefetch(k)                      # the next folder with images
+                        try:
+                            ply_name = os.path.basename(folder) + ".ply"
+                            out_path = os.path.join(folder, ply_name)
+                            _process_source(folder, out_path,
+                                            f"folder '{os.path.basename(folder)}'",
+                                            host=pending.pop(folder))
+                            success_count += 1
+                        except Exception as e:
+                            log(f"  ❌ Error in {os.path.basename(folder)}: {e}\n")
+                    else:
+                        log(f"  Skipping {os.path.basename(folder)} (No images found).")
 
             log(f"=== Batch Complete: {success_count}/{len(subfolders)} succeeded ===")
 

@@ -1,0 +1,67 @@
+#!/usr/bin/env python
+"""End-to-end file path of the drop-in: ``process_multi_ply(mode='batch')`` over C2 view folders
+of 8-bit PNG captures (PNG decode on a host thread pool with the next folder prefetched, H2D,
+fused kernels, native ASCII PLY writer).  Reported in DESIGN.md, never the bench metric.
+
+Prints one JSON line: seconds per view for the whole batch, and the serial cost of its parts
+(frame read + decode, reconstruct incl. H2D/D2H, PLY write) measured view by view.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--views", type=int, default=6)
+    args = ap.parse_args()
+
+    from structured_light_for_3d_model_replication_amd import calibration, synth
+    from structured_light_for_3d_model_replication_amd import processing as PR
+
+    rig = synth.default_rig(1920, 1080, 1920, 1080)
+    with tempfile.TemporaryDirectory() as tmp:
+        calib = os.path.join(tmp, "calib.mat")
+        calibration.save_mat(calib, rig.tables())
+        root = os.path.join(tmp, "scan")
+        for i in range(args.views):
+            v = synth.render_view(rig, 360.0 * i / args.views, seed=i, n_present=44)
+            synth.write_capture(v, os.path.join(root, f"obj_{i:02d}_scan"))
+        folders = sorted(os.path.join(root, d) for d in os.listdir(root))
+        kw = dict(n_sets_col=11, n_sets_row=10)
+        PR.ProcessingLogic.process_multi_ply(calib, folders[0], "single", log_callback=lambda m: None, **kw)  # warm-up
+        t0 = time.perf_counter()
+        PR.ProcessingLogic.process_multi_ply(calib, root, "batch", log_callback=lambda m: None, **kw)
+        batch_s = (time.perf_counter() - t0) / args.views
+
+        cfg = PR.E.DecodeConfig(1920, 1080, 11, 10, "otsu")
+        cal = calibration.load_mat(calib)
+        t_read = t_rec = t_ply = 0.0
+        pts = 0
+        for f in folders:
+            t = time.perf_counter(); host = PR.read_capture(f, cfg); t_read += time.perf_counter() - t
+            t = time.perf_counter()
+            dev, _ = PR.load_capture(f, cfg, host=host)
+            P, C = PR.reconstruct_view(dev, cfg, cal, 1, 2.0)
+            t_rec += time.perf_counter() - t
+            t = time.perf_counter(); PR.ProcessingLogic._save_ply(P, C, os.path.join(tmp, "x.ply")); t_ply += time.perf_counter() - t
+            pts += len(P)
+        n = len(folders)
+        print(json.dumps({"what": "process_multi_ply batch, C2 PNG folders (end to end)", "views": n,
+                          "points_per_view": pts // n, "s_per_view_batch": round(batch_s, 4),
+                          "s_per_view_parts": {"read_decode_png": round(t_read / n, 4),
+                                               "h2d_kernels_d2h": round(t_rec / n, 4),
+                                               "ply_write": round(t_ply / n, 4)},
+                          "host_cpus": os.cpu_count()}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
