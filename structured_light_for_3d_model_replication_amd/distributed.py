@@ -14,7 +14,6 @@ data path.  Two optional collectives exist for the end of a job:
 """
 from __future__ import annotations
 
-import glob
 import os
 
 import torch
@@ -43,10 +42,6 @@ def view_folders(target_path: str):
     """Batch-mode view folders in a deterministic order (the reference iterates
     ``os.scandir`` order, which is unspecified; sharding needs an order every rank agrees on)."""
     return sorted(f.path for f in os.scandir(target_path) if f.is_dir())
-
-
-def has_images(folder: str) -> bool:
-    return bool(glob.glob(os.path.join(folder, "*.bmp")) or glob.glob(os.path.join(folder, "*.png")))
 
 
 def batch_summary(success: int, total: int, device=None) -> tuple[int, int]:
@@ -97,34 +92,29 @@ def process_batch_sharded(calib_path, target_path, log_callback=None, process_so
         else:
             print(msg)
 
+    from . import processing as PR
+    folders = view_folders(target_path)
+    mine = shard(folders, rank, world)
     if process_source is None:
-        from . import processing as PR
+        # the single-process batch pipeline (prefetch read, GPU, writer thread) on this
+        # rank's block of folders
         import scipy.io
+        from . import engine as E
         data = scipy.io.loadmat(calib_path)
         calib = {k: data[k] for k in ("Nc", "Oc", "wPlaneCol", "wPlaneRow", "cam_K")}
         cfg_kw = {k: kw[k] for k in ("n_sets_col", "n_sets_row", "thresh_mode", "shadow_val",
                                      "contrast_val") if k in kw}
-        from . import engine as E
         cfg = E.DecodeConfig(1920, 1080, **cfg_kw)
-
-        def process_source(folder, out_path):
-            dev, _ = PR.load_capture(folder, cfg)
-            P, C = PR.reconstruct_view(dev, cfg, calib, kw.get("row_mode", 1), kw.get("epipolar_tol", 2.0))
-            PR.ProcessingLogic._save_ply(P, C, out_path)
-
-    folders = view_folders(target_path)
-    mine = shard(folders, rank, world)
-    ok = 0
-    for folder in mine:
-        if not has_images(folder):
-            log(f"  Skipping {os.path.basename(folder)} (No images found).")
-            continue
-        try:
-            process_source(folder, os.path.join(folder, os.path.basename(folder) + ".ply"))
-            ok += 1
-            log(f"  ✔ Saved: {os.path.basename(folder)}.ply")
-        except Exception as e:  # noqa: BLE001 - per-folder isolation like the reference
-            log(f"  ❌ Error in {os.path.basename(folder)}: {e}\n")
+        ok = PR.run_view_folders(
+            mine, log, PR.batch_reconstruct_stage(cfg, calib, kw.get("row_mode", 1),
+                                                  kw.get("epipolar_tol", 2.0), log),
+            read=lambda f: PR.read_capture(f, cfg), write=PR.batch_write_stage())
+    else:
+        def one(folder, _host):
+            name = os.path.basename(folder) + ".ply"
+            process_source(folder, os.path.join(folder, name))
+            log(f"  ✔ Saved: {name}")
+        ok = PR.run_view_folders(mine, log, one)
     dev = torch.device("cuda", torch.cuda.current_device()) if (
         dist.is_initialized() and dist.get_backend() == "nccl") else None
     total_ok, _ = batch_summary(ok, len(mine), dev)

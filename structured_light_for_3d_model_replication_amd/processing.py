@@ -70,6 +70,68 @@ def read_capture(source, cfg: E.DecodeConfig, order=("bmp", "png")):
     return stack, texture
 
 
+def has_images(folder: str) -> bool:
+    """Batch mode's folder filter (processing.py:320-321)."""
+    return bool(glob.glob(os.path.join(folder, "*.bmp")) or glob.glob(os.path.join(folder, "*.png")))
+
+
+def run_view_folders(subfolders, log, reconstruct, read=None, write=None) -> int:
+    """The per-folder loop of batch mode (processing.py:314-334) as a three-stage pipeline.
+
+    ``read(folder) -> host`` (frame read + PNG decode) runs one folder ahead on a prefetch
+    thread; ``reconstruct(folder, host) -> result`` (H2D, kernels, D2H) on the calling thread;
+    ``write(folder, result) -> out_name`` (ASCII PLY) on a writer thread while the next folder is
+    reconstructed.  At most one folder is in each stage.  Per-folder isolation as in the
+    reference: an exception in any stage is logged as ``❌ Error in <folder>`` at that folder's
+    turn and the loop goes on; folders without images are skipped.  Log order differs from the
+    serial loop only in that a folder's ``✔ Saved`` line comes after the next folder's first
+    progress lines.  Returns the number of folders that succeeded."""
+    from concurrent.futures import ThreadPoolExecutor
+    with_imgs = [f for f in subfolders if has_images(f)]
+    success = 0
+    with ThreadPoolExecutor(max_workers=1) as pre, ThreadPoolExecutor(max_workers=1) as wr:
+        pending = {}
+        writing = []
+
+        def prefetch(i):
+            if read is not None and i < len(with_imgs) and with_imgs[i] not in pending:
+                pending[with_imgs[i]] = pre.submit(read, with_imgs[i])
+
+        def drain():
+            nonlocal success
+            while writing:
+                folder, fut = writing.pop()
+                try:
+                    name = fut.result()
+                    success += 1
+                    log(f"  ✔ Saved: {name}\n")
+                except Exception as e:  # noqa: BLE001 - per-folder isolation like the reference
+                    log(f"  ❌ Error in {os.path.basename(folder)}: {e}\n")
+
+        prefetch(0)
+        k = 0
+        for folder in subfolders:
+            if not (k < len(with_imgs) and with_imgs[k] == folder):
+                log(f"  Skipping {os.path.basename(folder)} (No images found).")
+                continue
+            k += 1
+            prefetch(k)                                  # the next folder with images
+            try:
+                host = pending.pop(folder).result() if read is not None else None
+                result = reconstruct(folder, host)
+            except Exception as e:  # noqa: BLE001
+                drain()
+                log(f"  ❌ Error in {os.path.basename(folder)}: {e}\n")
+                continue
+            drain()
+            if write is None:
+                success += 1
+            else:
+                writing.append((folder, wr.submit(write, folder, result)))
+        drain()
+    return success
+
+
 def load_capture(source, cfg: E.DecodeConfig, order=("bmp", "png"), host=None):
     """Discover, decode and upload one capture: ``(DeviceFrames, texture)``.  ``host``: the
     result of :func:`read_capture` when it was already done (e.g. prefetched)."""
@@ -191,39 +253,36 @@ class ProcessingLogic:
             subfolders = [f.path for f in os.scandir(target_path) if f.is_dir()]
             log(f"Found {len(subfolders)} subfolders to process.")
 
-            # The next view folder's frames are read and decoded on a prefetch thread while
-            # this one is reconstructed and its PLY written; a read error surfaces (and is
-            # reported) at that folder's turn, as in the reference's per-folder try/except.
-            from concurrent.futures import ThreadPoolExecutor
-            with_imgs = [f for f in subfolders
-                         if glob.glob(os.path.join(f, "*.bmp")) or glob.glob(os.path.join(f, "*.png"))]
-            success_count = 0
-            with ThreadPoolExecutor(max_workers=1) as pre:
-                pending = {}
-
-                def prefetch(i):
-                    if i < len(with_imgs) and with_imgs[i] not in pending:
-                        pending[with_imgs[i]] = pre.submit(read_capture, with_imgs[i], cfg)
-
-                prefetch(0)
-                k = 0
-                for folder in subfolders:
-                    if k < len(with_imgs) and with_imgs[k] == folder:
-                        k += 1
-                        prefetch(k)                      # the next folder with images
-                        try:
-                            ply_name = os.path.basename(folder) + ".ply"
-                            out_path = os.path.join(folder, ply_name)
-                            _process_source(folder, out_path,
-                                            f"folder '{os.path.basename(folder)}'",
-                                            host=pending.pop(folder))
-                            success_count += 1
-                        except Exception as e:
-                            log(f"  ❌ Error in {os.path.basename(folder)}: {e}\n")
-                    else:
-                        log(f"  Skipping {os.path.basename(folder)} (No images found).")
-
+            # Pipelined: the next folder's frames are read on a prefetch thread and this
+            # folder's PLY is written on a writer thread while the following one is
+            # reconstructed (run_view_folders); errors stay per folder as in the reference.
+            success_count = run_view_folders(
+                subfolders, log, batch_reconstruct_stage(cfg, calib_data, row_mode, epipolar_tol, log),
+                read=lambda f: read_capture(f, cfg), write=batch_write_stage())
             log(f"=== Batch Complete: {success_count}/{len(subfolders)} succeeded ===")
+
+
+def batch_reconstruct_stage(cfg, calib, row_mode, epipolar_tol, log):
+    """``reconstruct`` stage of :func:`run_view_folders`: upload + fused kernels -> host cloud,
+    with the reference's progress lines (processing.py:264-272)."""
+    def stage(folder, host):
+        log(f"  -> Decoding folder '{os.path.basename(folder)}'  "
+            f"[col-sets={cfg.n_sets_col}  row-sets={cfg.n_sets_row}]...")
+        dev, _ = load_capture(folder, cfg, host=host)
+        log("  -> Reconstructing 3D points...")
+        points, colors = reconstruct_view(dev, cfg, calib, row_mode, epipolar_tol)
+        log(f"  -> Saving {len(points)} points...")
+        return points, colors
+    return stage
+
+
+def batch_write_stage():
+    """``write`` stage of :func:`run_view_folders`: ``<folder>/<folder name>.ply``."""
+    def stage(folder, result):
+        name = os.path.basename(folder) + ".ply"
+        ProcessingLogic._save_ply(result[0], result[1], os.path.join(folder, name))
+        return name
+    return stage
 
 
 def reconstruct_view(dev: E.DeviceFrames, cfg: E.DecodeConfig, calib: dict, row_mode=1,

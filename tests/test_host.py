@@ -161,3 +161,56 @@ def test_generate_patterns_is_gray_code():
     for b in range(11):
         assert np.array_equal(P[0][b], seq[2 + 2 * b])
         assert np.array_equal(P[1][b], seq[24 + 2 * b])
+
+
+def test_run_view_folders_pipeline(tmp_path):
+    """Batch-mode folder loop (processing.py:314-334) as read / reconstruct / write stages:
+    every folder processed once and in order, errors isolated per folder and per stage,
+    image-less folders skipped, a folder counted only after its PLY is written."""
+    import threading
+    from structured_light_for_3d_model_replication_amd import processing as PR
+    names = ["a", "b_readfail", "c", "empty", "d_gpufail", "e_writefail", "f"]
+    for n in names:
+        (tmp_path / n).mkdir()
+        if n != "empty":
+            (tmp_path / n / "00.png").write_bytes(b"x")
+    folders = [str(tmp_path / n) for n in names]
+    main = threading.get_ident()
+    seen = {"read": [], "rec": [], "write": []}
+
+    def read(f):
+        assert threading.get_ident() != main
+        seen["read"].append(os.path.basename(f))
+        if f.endswith("readfail"):
+            raise ValueError("Not enough images (got 3, need at least 4).")
+        return os.path.basename(f).upper()
+
+    def rec(f, host):
+        assert threading.get_ident() == main and host == os.path.basename(f).upper()
+        seen["rec"].append(os.path.basename(f))
+        if f.endswith("gpufail"):
+            raise RuntimeError("kernel failed")
+        return host
+
+    def write(f, res):
+        assert threading.get_ident() != main
+        seen["write"].append(res)
+        if f.endswith("writefail"):
+            raise OSError("disk full")
+        return os.path.basename(f) + ".ply"
+
+    logs = []
+    ok = PR.run_view_folders(folders, logs.append, rec, read=read, write=write)
+    assert ok == 3
+    assert seen["read"] == [n for n in names if n != "empty"]
+    assert seen["rec"] == ["a", "c", "d_gpufail", "e_writefail", "f"]
+    assert seen["write"] == ["A", "C", "E_WRITEFAIL", "F"]
+    assert [s.strip() for s in logs] == [
+        "✔ Saved: a.ply",
+        "❌ Error in b_readfail: Not enough images (got 3, need at least 4).",
+        "Skipping empty (No images found).",
+        "✔ Saved: c.ply",
+        "❌ Error in d_gpufail: kernel failed",
+        "❌ Error in e_writefail: disk full",
+        "✔ Saved: f.ply",
+    ]
