@@ -78,11 +78,30 @@ def imread_bgr(path) -> np.ndarray:
     return np.ascontiguousarray(a[..., 2::-1][..., :3], dtype=np.uint8)
 
 
-def load_frames(files, indices=None, workers: int = 8):
-    """Decode the given frames (grayscale) on a thread pool; returns a list of arrays."""
+def decode_threads() -> int:
+    """Host decode threads: ``SLG_DECODE_THREADS``, else the CPUs this process may use, at
+    most 16 (a GPU box's CPU share; more only contends with the PLY writer)."""
+    env = os.environ.get("SLG_DECODE_THREADS")
+    if env:
+        return max(1, int(env))
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 8
+    return max(1, min(16, n))
+
+
+def load_frames(files, indices=None, workers: int = 0, texture: bool = False):
+    """Decode the given frames (grayscale) on a thread pool; returns a list of arrays, plus
+    ``cv2.imread(files[0])`` (BGR texture, processing.py:124) decoded in the same pool when
+    ``texture`` — so the texture's second decode of frame 0 is not a serial tail."""
     idx = range(len(files)) if indices is None else indices
     paths = [files[i] for i in idx]
-    if len(paths) <= 1:
-        return [imread_gray(p) for p in paths]
-    with ThreadPoolExecutor(max_workers=min(workers, len(paths))) as ex:
-        return list(ex.map(imread_gray, paths))
+    workers = workers or decode_threads()
+    if len(paths) + texture <= 1:
+        imgs = [imread_gray(p) for p in paths]
+        return (imgs, imread_bgr(files[0])) if texture else imgs
+    with ThreadPoolExecutor(max_workers=min(workers, len(paths) + texture)) as ex:
+        tex = ex.submit(imread_bgr, files[0]) if texture else None   # first: the longest task
+        imgs = list(ex.map(imread_gray, paths))
+        return (imgs, tex.result()) if texture else imgs

@@ -62,11 +62,10 @@ def read_capture(source, cfg: E.DecodeConfig, order=("bmp", "png")):
     if len(files) < 4:
         raise ValueError(f"Not enough images (got {len(files)}, need at least 4).")
     need = _needed_frames(len(files), cfg) if cfg.variant == "processing" else list(range(len(files)))
-    imgs = FR.load_frames(files, need)
+    imgs, texture = FR.load_frames(files, need, texture=True)
     stack = [None] * len(files)
     for i, im in zip(need, imgs):
         stack[i] = im
-    texture = FR.imread_bgr(files[0])
     return stack, texture
 
 

@@ -67,8 +67,8 @@ class SLSystem:
         if len(files) < 4:
             raise ValueError("Not enough images in folder to decode.")
         cfg = E.DecodeConfig(1920, 1080, variant="slsystem")
-        imgs = PR.FR.load_frames(files)
-        dev = E.DeviceFrames(imgs, PR.FR.imread_bgr(files[0]))
+        imgs, tex = PR.FR.load_frames(files, texture=True)
+        dev = E.DeviceFrames(imgs, tex)
         print("Decoding Columns...")
         print("Decoding Rows...")
         print("Reconstructing 3D points...")
