@@ -23,6 +23,8 @@
  *   slg_reconstruct_batch  <- process_multi_ply(mode='batch') over view folders
  *                             (server/processing.py:314-334): many views, one stream
  *   slg_ply_write          <- ProcessingLogic._save_ply (server/processing.py:236-248), host side
+ *   slg_png_gray8_size /   <- cv2.imread(f, 0) of an 8-bit grayscale capture frame
+ *   slg_png_gray8_decode      (server/processing.py:59-60,98-99), host side fast path
  *   slg_rays_match_pinhole <- the `Nc.shape[1] == h*w` ray source test
  *                             (server/processing.py:143-156): tells whether the calibration's
  *                             Nc table equals the cam_K pinhole rays bit for bit, in which case
@@ -212,6 +214,15 @@ int32_t slg_rays_match_pinhole(const double *rays, int32_t height, int32_t width
  * (<= 0: all cores).  Returns bytes written, or -SLG_ERR_* on failure. */
 int64_t slg_ply_write(const char *path, const double *xyz, const uint8_t *bgr, int64_t n,
                       int32_t n_threads);
+
+/* Host: frame ingest fast path for cv2.imread(f, 0) (processing.py:59-60,98-99) on 8-bit
+ * grayscale, non-interlaced PNGs, where it is the identity on the stored samples.
+ * slg_png_gray8_size returns 0 and the size for such a file, non-zero for any other file
+ * (decode it the general way).  slg_png_gray8_decode fills out[height][width]; non-zero on a
+ * CRC error, a truncated stream or a size mismatch.  Thread-safe (one call per decode thread). */
+int32_t slg_png_gray8_size(const char *path, int32_t *width, int32_t *height);
+int32_t slg_png_gray8_decode(const char *path, uint8_t *out, int64_t cap, int32_t width,
+                             int32_t height);
 
 #ifdef __cplusplus
 }

@@ -8,6 +8,7 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "slgpu.hip")
+SRCS = [SRC, os.path.join(PKG, "csrc", "png_gray.cpp")]
 HDR = os.path.join(ROOT, "include", "slgpu.h")
 OUT = os.path.join(PKG, "libslgpu.so")
 
@@ -19,13 +20,14 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in (SRC, HDR, __file__))
+    return any(os.path.getmtime(p) > t for p in (*SRCS, HDR, __file__))
 
 
 def build_native(force: bool = False, verbose: bool = False) -> str:
-    """Compile ``csrc/slgpu.hip`` into ``libslgpu.so`` (skipped when up to date)."""
+    """Compile ``csrc/slgpu.hip`` (+ the host PNG fast path) into ``libslgpu.so`` (skipped when
+    up to date)."""
     if force or needs_build():
-        cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", SRC]
+        cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *SRCS, "-lz", "-ldl"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -57,8 +57,29 @@ def _to_gray(im, path) -> np.ndarray:
     return y.astype(np.uint8)
 
 
+def _png_gray8(path):
+    """Native fast path (``slg_png_gray8_*``): an 8-bit grayscale PNG decoded without PIL;
+    ``None`` for any other file (decoded the general way below)."""
+    if not str(path).lower().endswith(".png") or os.environ.get("SLG_PNG_PIL"):
+        return None
+    import ctypes
+    from . import _native as N
+    L = N.lib()
+    bp = os.fsencode(path)
+    w, h = ctypes.c_int32(), ctypes.c_int32()
+    if L.slg_png_gray8_size(bp, ctypes.byref(w), ctypes.byref(h)) != 0:
+        return None
+    out = np.empty((h.value, w.value), dtype=np.uint8)
+    if L.slg_png_gray8_decode(bp, out.ctypes.data_as(ctypes.c_void_p), out.size, w, h) != 0:
+        return None
+    return out
+
+
 def imread_gray(path) -> np.ndarray:
     """``cv2.imread(path, 0)``; raises like ``None.astype`` would for unreadable files."""
+    a = _png_gray8(path)
+    if a is not None:
+        return a
     im = _open(path)
     if im is None:
         raise AttributeError("'NoneType' object has no attribute 'astype'")
@@ -67,6 +88,9 @@ def imread_gray(path) -> np.ndarray:
 
 def imread_bgr(path) -> np.ndarray:
     """``cv2.imread(path)``: HxWx3 BGR uint8 (grayscale replicated)."""
+    a = _png_gray8(path)
+    if a is not None:
+        return np.repeat(a[..., None], 3, axis=-1)
     im = _open(path)
     if im is None:
         raise AttributeError("'NoneType' object has no attribute 'reshape'")

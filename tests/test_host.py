@@ -214,3 +214,76 @@ def test_run_view_folders_pipeline(tmp_path):
         "❌ Error in e_writefail: disk full",
         "✔ Saved: f.ply",
     ]
+
+
+def _png_bytes(img, filters, interlace=0, depth=8, ctype=0, corrupt=False):
+    """A PNG written by hand with the given per-row filter types (PNG spec §9 filters)."""
+    import struct
+    import zlib
+    h, w = img.shape
+    raw = bytearray()
+    prev = np.zeros(w, np.int32)
+    for y in range(h):
+        cur = img[y].astype(np.int32)
+        left = np.concatenate([[0], cur[:-1]])
+        ul = np.concatenate([[0], prev[:-1]])
+        f = filters[y % len(filters)]
+        if f == 0:
+            pred = np.zeros(w, np.int32)
+        elif f == 1:
+            pred = left
+        elif f == 2:
+            pred = prev
+        elif f == 3:
+            pred = (left + prev) >> 1
+        else:
+            p = left + prev - ul
+            pa, pb, pc = abs(p - left), abs(p - prev), abs(p - ul)
+            pred = np.where((pa <= pb) & (pa <= pc), left, np.where(pb <= pc, prev, ul))
+        raw += bytes([f]) + ((cur - pred) & 255).astype(np.uint8).tobytes()
+        prev = cur
+
+    def chunk(t, d):
+        crc = zlib.crc32(t + d) ^ (1 if corrupt and t == b"IDAT" else 0)
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", crc & 0xffffffff)
+    ihdr = struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, interlace)
+    return (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"tEXt", b"k\x00v")
+            + chunk(b"IDAT", zlib.compress(bytes(raw))[:20]) + chunk(b"IDAT", zlib.compress(bytes(raw))[20:])
+            + chunk(b"IEND", b""))
+
+
+def test_png_gray8_fast_path_matches_general_decoder(tmp_path):
+    """Native PNG ingest (slg_png_gray8_*): every row filter, split IDATs, ancillary chunks;
+    identical to the general (PIL) decoder; other formats and corrupt files fall back."""
+    from PIL import Image
+    from structured_light_for_3d_model_replication_amd import build, frames as FR
+    build.build_native()
+    rng = np.random.default_rng(5)
+    for (h, w) in ((23, 37), (1, 1), (64, 5)):
+        img = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        img[: h // 2] = np.clip(img[: h // 2] // 8 + np.arange(w) * 3, 0, 255)   # some smooth rows
+        for filters in ((0,), (1,), (2,), (3,), (4,), (4, 3, 2, 1, 0)):
+            p = tmp_path / f"f{h}_{w}_{''.join(map(str, filters))}.png"
+            p.write_bytes(_png_bytes(img, filters))
+            fast = FR._png_gray8(str(p))
+            assert fast is not None and np.array_equal(fast, img)
+            assert np.array_equal(np.asarray(Image.open(p)), img)
+            assert np.array_equal(FR.imread_gray(str(p)), img)
+            assert np.array_equal(FR.imread_bgr(str(p)), np.repeat(img[..., None], 3, -1))
+    # PIL-written capture frames (synthetic renderer's writer)
+    a = rng.integers(0, 256, (40, 60), dtype=np.uint8)
+    Image.fromarray(a).save(tmp_path / "pil.png")
+    assert np.array_equal(FR._png_gray8(str(tmp_path / "pil.png")), a)
+    # not handled here: colour, 16-bit, interlaced, corrupt -> general decoder
+    Image.fromarray(np.stack([a] * 3, -1)).save(tmp_path / "rgb.png")
+    Image.fromarray(a.astype(np.uint16) * 257).save(tmp_path / "g16.png")
+    (tmp_path / "il.png").write_bytes(_png_bytes(a, (0,), interlace=1))
+    (tmp_path / "bad.png").write_bytes(_png_bytes(a, (1,), corrupt=True))
+    (tmp_path / "trunc.png").write_bytes(_png_bytes(a, (1,))[:-30])
+    for n in ("rgb", "g16", "il", "bad", "trunc"):
+        assert FR._png_gray8(str(tmp_path / f"{n}.png")) is None, n
+    assert FR._png_gray8(str(tmp_path / "missing.png")) is None
+    assert np.array_equal(FR.imread_gray(str(tmp_path / "rgb.png")),
+                          FR._to_gray(Image.open(tmp_path / "rgb.png"), "rgb.png"))
+    with pytest.raises(AttributeError):
+        FR.imread_gray(str(tmp_path / "missing.png"))
