@@ -198,6 +198,36 @@ def test_process_multi_ply_batch(tmp_path, mods):
     assert logs[-1].startswith("=== Batch Complete: 2/4 succeeded")
 
 
+def test_sharded_batch_single_process(tmp_path, mods):
+    """The multi-GPU batch entry (``distributed.process_batch_sharded``) with no process group:
+    the same read / GPU / write pipeline as batch mode, PLY bytes equal to the oracle's, a
+    bad folder isolated, the job-wide summary line last."""
+    E, PR, N = mods
+    from structured_light_for_3d_model_replication_amd import synth, calibration, distributed as D
+    rig = synth.default_rig(160, 120, 1920, 1080)
+    calibration.save_mat(str(tmp_path / "calib.mat"), rig.tables())
+    root = tmp_path / "obj"
+    views = {}
+    for k, ang in enumerate((0.0, 120.0, 240.0)):
+        v = synth.render_view(rig, ang, seed=200 + k)
+        d = root / f"v{k}"
+        synth.write_capture(v, str(d))
+        views[d] = v
+    synth.write_capture(synth.render_view(rig, 0.0, seed=9, n_present=3), str(root / "bad"))
+    logs = []
+    ok = D.process_batch_sharded(str(tmp_path / "calib.mat"), str(root), log_callback=logs.append,
+                                 n_sets_col=11, n_sets_row=11, row_mode=1)
+    assert ok == 3
+    cal = calibration.load_mat(str(tmp_path / "calib.mat"))
+    for d, v in views.items():
+        c, r, m = O.decode_processing(list(v.frames), n_sets_col=11, n_sets_row=11)
+        tex = np.repeat(v.frames[0][..., None], 3, -1)
+        P, C = O.reconstruct_processing(c, r, m, tex, cal, row_mode=1)
+        assert (d / f"{d.name}.ply").read_bytes() == O.ply_bytes(P, C)
+    assert any("Error in bad" in s and "Not enough images" in s for s in logs)
+    assert logs[-1] == "=== Batch Complete: 3/4 succeeded ==="
+
+
 def test_generate_cloud_legacy(tmp_path, mods, capsys):
     E, PR, N = mods
     from structured_light_for_3d_model_replication_amd import synth, calibration
