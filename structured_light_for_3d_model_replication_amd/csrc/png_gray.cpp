@@ -34,6 +34,8 @@ bool read_file(const char* path, std::vector<uint8_t>& buf) {
   return ok;
 }
 
+uint32_t chunk_crc(const uint8_t* p, size_t n);
+
 struct Png {
   uint32_t w = 0, h = 0;
   std::vector<uint8_t> idat;                  // concatenated zlib stream
@@ -52,7 +54,7 @@ int parse(const std::vector<uint8_t>& b, Png& png, bool want_data) {
     const uint8_t* data = &b[o + 8];
     const uint32_t crc = be32(&b[o + 8 + len]);
     const bool critical = !(type[0] & 0x20);
-    if (critical && uint32_t(crc32(crc32(0L, Z_NULL, 0), type, len + 4)) != crc) return kInvalid;
+    if (critical && chunk_crc(type, size_t(len) + 4) != crc) return kInvalid;
     if (!memcmp(type, "IHDR", 4)) {
       if (len != 13) return kInvalid;
       png.w = be32(data);
@@ -79,10 +81,12 @@ int parse(const std::vector<uint8_t>& b, Png& png, bool want_data) {
 using ld_alloc_t = void* (*)();
 using ld_free_t = void (*)(void*);
 using ld_zlib_t = int (*)(void*, const void*, size_t, void*, size_t, size_t*);
+using ld_crc_t = uint32_t (*)(uint32_t, const void*, size_t);
 struct Deflate {
   ld_alloc_t alloc = nullptr;
   ld_free_t free = nullptr;
   ld_zlib_t zlib = nullptr;
+  ld_crc_t crc = nullptr;                      // carry-less-multiply CRC-32 (~10x zlib 1.2.11's)
 };
 
 const Deflate& deflate_lib() {
@@ -95,9 +99,16 @@ const Deflate& deflate_lib() {
     d.alloc = reinterpret_cast<ld_alloc_t>(dlsym(h, "libdeflate_alloc_decompressor"));
     d.free = reinterpret_cast<ld_free_t>(dlsym(h, "libdeflate_free_decompressor"));
     d.zlib = reinterpret_cast<ld_zlib_t>(dlsym(h, "libdeflate_zlib_decompress"));
-    if (!d.alloc || !d.free || !d.zlib) d = Deflate{};
+    d.crc = reinterpret_cast<ld_crc_t>(dlsym(h, "libdeflate_crc32"));
+    if (!d.alloc || !d.free || !d.zlib || !d.crc) d = Deflate{};
   });
   return d;
+}
+
+uint32_t chunk_crc(const uint8_t* p, size_t n) {
+  const Deflate& d = deflate_lib();
+  if (d.crc) return d.crc(0, p, n);
+  return uint32_t(crc32(crc32(0L, Z_NULL, 0), p, uInt(n)));
 }
 
 bool inflate_all(const std::vector<uint8_t>& in, uint8_t* out, size_t n_out) {
