@@ -57,6 +57,15 @@ def _to_gray(im, path) -> np.ndarray:
     return y.astype(np.uint8)
 
 
+def _is_png_gray8(path) -> bool:
+    if not str(path).lower().endswith(".png") or os.environ.get("SLG_PNG_PIL"):
+        return False
+    import ctypes
+    from . import _native as N
+    w, h = ctypes.c_int32(), ctypes.c_int32()
+    return N.lib().slg_png_gray8_size(os.fsencode(path), ctypes.byref(w), ctypes.byref(h)) == 0
+
+
 def _png_gray8(path):
     """Native fast path (``slg_png_gray8_*``): an 8-bit grayscale PNG decoded without PIL;
     ``None`` for any other file (decoded the general way below)."""
@@ -125,7 +134,14 @@ def load_frames(files, indices=None, workers: int = 0, texture: bool = False):
     if len(paths) + texture <= 1:
         imgs = [imread_gray(p) for p in paths]
         return (imgs, imread_bgr(files[0])) if texture else imgs
+    # An 8-bit gray PNG frame 0 that is decoded anyway gives the texture by replication (what
+    # cv2.imread(f) returns for it) instead of a second decode.
+    reuse = texture and files[0] in paths and _is_png_gray8(files[0])
     with ThreadPoolExecutor(max_workers=min(workers, len(paths) + texture)) as ex:
-        tex = ex.submit(imread_bgr, files[0]) if texture else None   # first: the longest task
+        tex = ex.submit(imread_bgr, files[0]) if texture and not reuse else None  # longest task first
         imgs = list(ex.map(imread_gray, paths))
-        return (imgs, tex.result()) if texture else imgs
+        if not texture:
+            return imgs
+        if reuse:
+            return imgs, np.repeat(imgs[paths.index(files[0])][..., None], 3, axis=-1)
+        return imgs, tex.result()
