@@ -31,6 +31,9 @@
 #include <stdlib.h>
 #include <math.h>
 #include <string>
+#include <errno.h>
+#include <fcntl.h>
+#include <unistd.h>
 #include <thread>
 #include <vector>
 
@@ -1935,14 +1938,38 @@ int64_t slg_ply_write(const char* path, const double* xyz, const uint8_t* bgr, i
   for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
   work(0);
   for (auto& x : th) x.join();
-  FILE* f = fopen(path, "wb");
-  if (!f) return -fail(SLG_ERR_INVALID, "cannot open %s", path);
-  int64_t total = fprintf(f, "ply\nformat ascii 1.0\nelement vertex %lld\nproperty float x\nproperty float y\n"
-                             "property float z\nproperty uchar red\nproperty uchar green\nproperty uchar blue\n"
-                             "end_header\n", (long long)n);
-  for (auto& p : parts) total += int64_t(fwrite(p.data(), 1, p.size(), f));
-  if (fclose(f) != 0) return -fail(SLG_ERR_INVALID, "write failed: %s", path);
-  return total;
+  char hdr[320];
+  const int hlen = snprintf(hdr, sizeof(hdr), "ply\nformat ascii 1.0\nelement vertex %lld\nproperty float x\n"
+                            "property float y\nproperty float z\nproperty uchar red\nproperty uchar green\n"
+                            "property uchar blue\nend_header\n", (long long)n);
+  // Each thread's part goes to its own offset with pwrite, in parallel (no serial copy through
+  // a stdio buffer: ~45 MB per C2 view).
+  std::vector<int64_t> off(size_t(nt) + 1);
+  off[0] = hlen;
+  for (int t = 0; t < nt; ++t) off[size_t(t) + 1] = off[size_t(t)] + int64_t(parts[size_t(t)].size());
+  const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+  if (fd < 0) return -fail(SLG_ERR_INVALID, "cannot open %s", path);
+  auto put = [fd](const char* b, int64_t len, int64_t at) {
+    while (len > 0) {
+      const ssize_t w = pwrite(fd, b, size_t(len), off_t(at));
+      if (w < 0 && errno == EINTR) continue;
+      if (w <= 0) return false;
+      b += w; len -= w; at += w;
+    }
+    return true;
+  };
+  std::vector<char> ok(size_t(nt) + 1, 1);
+  ok[size_t(nt)] = put(hdr, hlen, 0);
+  th.clear();
+  for (int t = 1; t < nt; ++t)
+    th.emplace_back([&, t] { ok[size_t(t)] = put(parts[size_t(t)].data(), int64_t(parts[size_t(t)].size()), off[size_t(t)]); });
+  ok[0] = put(parts[0].data(), int64_t(parts[0].size()), off[0]);
+  for (auto& x : th) x.join();
+  const bool closed = close(fd) == 0;
+  for (char c : ok)
+    if (!c) return -fail(SLG_ERR_INVALID, "write failed: %s", path);
+  if (!closed) return -fail(SLG_ERR_INVALID, "write failed: %s", path);
+  return off[size_t(nt)];
 }
 
 int32_t slg_reconstruct_batch(const slg_capture* caps, int32_t n_views, const slg_decode_params* dp,
