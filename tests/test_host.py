@@ -287,3 +287,23 @@ def test_png_gray8_fast_path_matches_general_decoder(tmp_path):
                           FR._to_gray(Image.open(tmp_path / "rgb.png"), "rgb.png"))
     with pytest.raises(AttributeError):
         FR.imread_gray(str(tmp_path / "missing.png"))
+
+
+def test_read_capture_native_png_matches_general_decoder(tmp_path, monkeypatch):
+    """Frame ingest of a capture folder (processing.py:49-60,98-99,124): the native PNG path
+    (texture replicated from frame 0's gray decode) equals the general PIL path exactly."""
+    from structured_light_for_3d_model_replication_amd import build, synth, engine as E
+    from structured_light_for_3d_model_replication_amd import processing as PR, frames as FR
+    build.build_native()
+    rig = synth.default_rig(96, 64, 1920, 1080)
+    v = synth.render_view(rig, 40.0, seed=3, n_present=20)
+    synth.write_capture(v, str(tmp_path / "cap"))
+    cfg = E.DecodeConfig(1920, 1080, 11, 11, "otsu")
+    stack, tex = PR.read_capture(str(tmp_path / "cap"), cfg)
+    monkeypatch.setenv("SLG_PNG_PIL", "1")
+    stack2, tex2 = PR.read_capture(str(tmp_path / "cap"), cfg)
+    assert np.array_equal(tex, tex2) and tex.shape == (64, 96, 3) and tex.dtype == np.uint8
+    assert all((a is None and b is None) or np.array_equal(a, b) for a, b in zip(stack, stack2))
+    assert np.array_equal(stack[0], v.frames[0])
+    monkeypatch.setenv("SLG_DECODE_THREADS", "3")
+    assert FR.decode_threads() == 3
