@@ -954,6 +954,9 @@ constexpr int kMaxViews = 16;
 #ifndef SLG_STAGED_STORES
 #define SLG_STAGED_STORES 0                // 1: phase D via LDS-packed contiguous stores (measured 355 vs 347 us per launch)
 #endif
+#ifndef SLG_PRIO
+#define SLG_PRIO 0                         // A/B: 1 = wave priority 2 in phase A, 0 after; 2 = 0 in A, 2 after
+#endif
 #ifndef SLG_M3_WAVES
 #define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
 #endif
@@ -1148,6 +1151,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     for (int i = tid; i < 512; i += kB) s_hn[i] = 0;   // ordered before phase C by block_scan's barrier
   }
   // ------------------------------------------------------------ A: decode + tile compaction
+  if (SLG_PRIO == 1) __builtin_amdgcn_s_setprio(2);
   int n_items;
   {
     uint32_t tex[6] = {0, 0, 0, 0, 0, 0};
@@ -1179,6 +1183,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     }
   }
   __syncthreads();
+  if (SLG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+  if (SLG_PRIO == 2) __builtin_amdgcn_s_setprio(2);
 
   stamp(0);
   // ------------------------------------------------------------ B: triangulate, balanced
