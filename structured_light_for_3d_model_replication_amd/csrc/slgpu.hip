@@ -954,6 +954,9 @@ constexpr int kMaxViews = 16;
 #ifndef SLG_STAGED_STORES
 #define SLG_STAGED_STORES 0                // 1: phase D via LDS-packed contiguous stores (measured 355 vs 347 us per launch)
 #endif
+#ifndef SLG_NT_STORES
+#define SLG_NT_STORES 0                    // A/B: 1 = phase-D cloud stores non-temporal
+#endif
 #ifndef SLG_PRIO
 #define SLG_PRIO 0                         // A/B: 1 = wave priority 2 in phase A, 0 after; 2 = 0 in A, 2 after
 #endif
@@ -1358,9 +1361,18 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       }
       if ((km[s][i] >> lane) & 1ull) {
         const int64_t q = base + before + __popcll(km[s][i] & lt);
-        gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
         const uint32_t c = s_bgr[tid + kB * i];
-        gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
+        if (SLG_NT_STORES) {
+          __builtin_nontemporal_store(pts[s][i][0], &gx[3 * q]);
+          __builtin_nontemporal_store(pts[s][i][1], &gx[3 * q + 1]);
+          __builtin_nontemporal_store(pts[s][i][2], &gx[3 * q + 2]);
+          __builtin_nontemporal_store(uint8_t(c), &gb[3 * q]);
+          __builtin_nontemporal_store(uint8_t(c >> 8), &gb[3 * q + 1]);
+          __builtin_nontemporal_store(uint8_t(c >> 16), &gb[3 * q + 2]);
+        } else {
+          gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
+          gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
+        }
       }
       base += round;
     }
