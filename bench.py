@@ -1,19 +1,24 @@
 #!/usr/bin/env python
 """Benchmark: decoded+triangulated Mpoints/s of the structured-light hot path on MI355X.
 
-Workload (BASELINE.json configs[1], "C2"): one 1920x1080 view per step, 11 column + 10 row
-Gray-code bits with inverses + white/black (44 frames), Otsu mask, row_mode 1 (epipolar
-filter, tol 2.0), fp32 XYZ + BGR out.  Every step does the full path for its view, inputs
-resident in HBM: the stats pass (histograms -> Otsu thresholds) and the fused
-decode/triangulate/compaction pass.  Steps rotate over a pool of distinct rendered turntable
-views (12 x 95 MB frame stacks > 256 MiB Infinity Cache) so frames stream from HBM.  Views are
-issued in batches (C3/C5 style): one fused main3 launch per batch of up to 16 views.  Default
---pipeline fused: batch k's fused launch also computes batch k+2's Otsu histograms (per-tile
-partials) and a small kernel on a side stream turns them into thresholds beside batch k+1's
-launch; the first two batches of a run get a regular stats pass (BatchReconstructor.
-run_pipelined).  --pipeline overlap: a separate stats pass of batch k+1 on a side stream;
---pipeline serial: stats + fused launch per batch on one stream (slg_reconstruct_batch).  One process per GPU (torchrun); each rank renders its own
-views (weak scaling, no data-path collective); value = all ranks' points / max-over-ranks time.
+Workload (BASELINE.json configs[1], "C2"): 1920x1080 views, 11 column + 10 row Gray-code bits
+with inverses + white/black (44 frames), Otsu mask, row_mode 1 (epipolar filter, tol 2.0),
+fp32 XYZ + BGR out, inputs resident in HBM.  A STEP is one batch of B views (default 12) through
+the whole path: ONE fused decode/triangulate/compaction launch over the batch, plus its Otsu
+thresholds -- in the default ``--pipeline fused`` the launch of batch k also counts batch k+2's
+histograms (per-tile partials) and a small kernel on a side stream turns them into thresholds
+beside batch k+1's launch (BatchReconstructor.run_pipelined).  The pipeline runs continuously
+from the priming stats passes (outside any timing) through the W warmup steps into the K timed
+steps, so every timed step is a steady-state step whatever K is.  Steps rotate over a pool of
+distinct rendered turntable views (views x copies HBM buffers, > 256 MiB Infinity Cache), so
+frames stream from HBM and a carried batch is never the batch being decoded.
+
+``--config c3``: the 36-view turntable scan (BASELINE configs[2]) as ONE job, views sharded
+across the ranks (strong scaling): every rank decodes its block, the clouds are gathered to rank
+0 through the C-ABI RCCL gatherv (``slg_gather_*``), the timed region includes it.
+``--config c4|c5``: the larger single-GPU geometries.  For N>1 on the default config each rank
+runs its own stream of views (weak scaling, no data-path collective); value = all ranks' points /
+max-over-ranks time.
 
 Prints ONE JSON line on stdout (rank 0).  Diagnostics go to stderr.
 """
@@ -22,6 +27,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import platform
+import subprocess
 import sys
 import time
 
@@ -29,7 +36,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "decoded+triangulated Mpoints/sec (1 GPU & 8-GPU node); % of HBM roofline"
-HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 measured copy)
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.3 measured copy)
+CPU_SHARE = 16             # host CPUs per GPU on the GPU box (gpurun: size pools to 16)
 
 
 def log(*a):
@@ -37,10 +45,13 @@ def log(*a):
 
 
 # Workloads (BASELINE.json configs / SURVEY §8(d)).  c2 is the metric's configuration and the
-# default; c4 / c5 are the larger single-view geometries, run on request (--config).
+# default; the others run on request (--config).
 CONFIGS = {
     "c2": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 10), n_present=44, views=12, copies=3, batch=12,
                text="C2: 1920x1080 view, 11 col + 10 row Gray bits + inverses + white/black (44 frames)"),
+    "c3": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 11), n_present=None, views=36, copies=1, batch=12,
+               text="C3: 36-view 360-degree turntable scan at 1920x1080, 11 col + 11 row Gray bits + "
+                    "inverses + white/black (46 frames), views sharded over the ranks, clouds gathered to rank 0"),
     "c4": dict(cam=(6000, 4000), proj=(3840, 2160), nsets=(12, 12), n_present=None, views=2, copies=2, batch=2,
                text="C4: 6000x4000 view, projector 3840x2160, 12 col + 12 row Gray bits + inverses + "
                     "white/black (50 frames)"),
@@ -50,25 +61,70 @@ CONFIGS = {
 }
 
 
-def cpu_baseline(views, cal, seconds, wl):
-    """Oracle (NumPy port of the reference path) on this host, one thread, frames in memory."""
-    import numpy as np
+# ----------------------------------------------------------------------------- CPU baseline
+_CPU_JOB = None     # (views, calib, proj, nsets): inherited by the forked workers, never pickled
+
+
+def _cpu_worker(args):
+    """One host process: the oracle over views until `seconds` elapse -> (points, views, s)."""
+    os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import sl_oracle as O
-    (PW, PH), (nc, nr) = wl["proj"], wl["nsets"]
+    seconds, first = args
+    views, cal, proj, nsets = _CPU_JOB
+    (PW, PH), (nc, nr) = proj, nsets
     done, pts, t0 = 0, 0, time.perf_counter()
     while True:
-        v = views[done % len(views)]
+        v = views[(first + done) % len(views)]
         col, row, mask = O.decode_processing(list(v.frames), n_cols=PW, n_rows=PH, n_sets_col=nc, n_sets_row=nr)
         P, _ = O.reconstruct_processing(col, row, mask, v.texture, cal, row_mode=1)
         pts += len(P)
         done += 1
         if time.perf_counter() - t0 >= seconds:
             break
-    dt = time.perf_counter() - t0
-    return {"value": round(pts / dt / 1e6, 4), "unit": "Mpoints/s", "cores": 1, "kind": "port",
-            "sample": f"{done} {wl['text'].split(':')[0]} views ({wl['cam'][0]}x{wl['cam'][1]}, "
-                      f"{nc}+{nr} bits, Otsu, row_mode 1), frames in "
-                      f"memory, oracle/sl_oracle.py NumPy restatement, 1 thread, {dt:.1f} s"}
+    return pts, done, time.perf_counter() - t0
+
+
+def _cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(views, cal, seconds, wl):
+    """The oracle (NumPy restatement of the reference path, test infrastructure) on this host,
+    frames in memory: (i) one process, (ii) a process pool with one stream of views per worker
+    on the box's CPU share.  Runs BEFORE the GPU is touched (fork-safe).  `value` is the pool
+    figure, the stronger baseline."""
+    global _CPU_JOB
+    import multiprocessing as mp
+    import numpy as np
+    _CPU_JOB = (views, cal, wl["proj"], wl["nsets"])
+    nsets = wl["nsets"]
+    one = _cpu_worker((seconds, 0))
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    workers = max(1, min(avail, CPU_SHARE))
+    with mp.get_context("fork").Pool(workers) as pool:
+        res = pool.map(_cpu_worker, [(seconds, w) for w in range(workers)])
+    pts = sum(r[0] for r in res)
+    n_views = sum(r[1] for r in res)
+    wall = max(r[2] for r in res)
+    tag = wl["text"].split(":")[0]
+    return {"value": round(pts / wall / 1e6, 4), "unit": "Mpoints/s", "cores": workers, "kind": "port",
+            "sample": f"{n_views} {tag} views ({wl['cam'][0]}x{wl['cam'][1]}, {nsets[0]}+{nsets[1]} bits, Otsu, "
+                      f"row_mode 1) on {workers} worker processes x ~{seconds:.0f} s, frames in memory, "
+                      "oracle/sl_oracle.py NumPy restatement of server/processing.py:28-234",
+            "single_process_value": round(one[0] / one[2] / 1e6, 4),
+            "single_process_sample": f"{one[1]} views in {one[2]:.1f} s, 1 process",
+            "host_cpus": os.cpu_count(), "cpus_available": avail, "cpu_model": _cpu_model(),
+            "numpy": np.__version__}
 
 
 def load_traffic_per_view():
@@ -87,8 +143,8 @@ def load_traffic_per_view():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1200)
-    ap.add_argument("--warmup", type=int, default=24)
+    ap.add_argument("--steps", type=int, default=100, help="timed steps (one fused batch launch each)")
+    ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
                     help="workload (default c2, the metric's configuration)")
     ap.add_argument("--views", type=int, default=None, help="distinct rendered views")
@@ -99,13 +155,17 @@ def main():
                     help="serial: stats + fused launch per batch on one stream; overlap: the next "
                          "batch's stats on a side stream during this batch's fused launch; fused: "
                          "batch k's fused launch computes batch k+2's histograms")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
     args = ap.parse_args()
     wl = CONFIGS[args.config]
     for k in ("views", "copies", "batch"):
         if getattr(args, k) is None:
             setattr(args, k, wl[k])
+    if args.config == "c3":
+        import bench_c3
+        return bench_c3.main(args, wl)
 
     import numpy as np
     import torch
@@ -114,12 +174,8 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
 
-    from structured_light_for_3d_model_replication_amd import engine as E, synth, _native
+    from structured_light_for_3d_model_replication_amd import synth
 
     (W, H), (PW, PH), (NC, NR) = wl["cam"], wl["proj"], wl["nsets"]
     rig = synth.default_rig(W, H, PW, PH)
@@ -128,6 +184,18 @@ def main():
     views = [synth.render_view(rig, view_deg=(rank * args.views + i) * 360.0 / (world * args.views),
                                seed=1000 * rank + i, n_present=wl["n_present"]) for i in range(args.views)]
     log(f"[rank {rank}] rendered {len(views)} views in {time.perf_counter() - t:.1f}s")
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:   # before the GPU is touched
+        t = time.perf_counter()
+        cpu = cpu_baseline(views, cal, args.cpu_seconds, wl)
+        log(f"[rank 0] cpu baseline {cpu['value']} Mpts/s on {cpu['cores']} processes "
+            f"({cpu['single_process_value']} on 1) in {time.perf_counter() - t:.1f}s")
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    from structured_light_for_3d_model_replication_amd import engine as E
 
     cfg = E.DecodeConfig(PW, PH, NC, NR, "otsu")
     row_mode, tol, f64 = 1, 2.0, args.xyz == "f64"
@@ -137,68 +205,68 @@ def main():
     dframes = [E.DeviceFrames(list(v.frames), v.texture, device=dev) for _ in range(args.copies) for v in views]
     P = len(dframes)
     dcal = E.DeviceCalib(cal, H, W, device=dev)
-    B = max(1, min(args.batch, E.MAX_VIEWS_PER_LAUNCH))
+    B = max(1, min(args.batch, E.MAX_VIEWS_PER_LAUNCH, P))
     s_main = torch.cuda.Stream(device=dev)
     s_stats = torch.cuda.Stream(device=dev)
     beng = E.BatchReconstructor(H, W, B, device=dev, slots=2)
     clouds = [[E.Cloud(H * W, row_mode, f64, device=dev) for _ in range(B)] for _ in range(2)]
     preps = {}
 
-    def prep(start, n, slot):
-        """Batch of n consecutive pool views from `start` on workspace/cloud slot `slot`."""
-        key = (start, n, slot)
+    def prep(start, slot):
+        """Batch of B consecutive pool views from `start` on workspace/cloud slot `slot`."""
+        key = (start % P, slot)
         if key not in preps:
-            fr = [dframes[(start + k) % P] for k in range(n)]
-            preps[key] = beng.prepare(fr, cfg, dcal, clouds[slot][:n], row_mode, tol, slot=slot)
+            fr = [dframes[(start + k) % P] for k in range(B)]
+            preps[key] = beng.prepare(fr, cfg, dcal, clouds[slot], row_mode, tol, slot=slot)
         return preps[key]
 
-    # points per view: one sanity pass over the pool in batches of B (same launch shape as timed)
+    # Reference counts: every pool view once through the plain (non-pipelined) batch path.
     pts = []
     for v0 in range(0, P, B):
-        n = min(B, P - v0)
-        beng.run(prep(v0, n, 0), stream=s_main)
+        pb = prep(v0, 0)
+        beng.run(pb, stream=s_main)
         s_main.synchronize()
-        pts += [int(clouds[0][k].count.item()) for k in range(n)]
-
-    def batches_for(first, count):
-        """Steps [first, first+count) as batches of <= B views on alternating slots."""
-        out, j = [], 0
-        while j < count:
-            n = min(B, count - j)
-            out.append(prep((first + j) % P, n, len(out) % 2))
-            j += n
-        return out
+        pts += [int(clouds[0][k].count.item()) for k in range(B)]
+    pts = pts[:P]
 
     K, Wm = args.steps, args.warmup
-    warm = batches_for(0, Wm)
-    timed = batches_for(Wm, K)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in timed]
+    # the whole run as ONE batch stream: warmup + timed + 2 look-ahead batches whose thresholds
+    # the last timed launches prepare (carried histograms), as every other step does
+    batches = [prep(b * B, b % 2) for b in range(Wm + K + 2)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     for a, b in ev:                                  # materialise the HIP events
         a.record(s_main)
         b.record(s_main)
     torch.cuda.synchronize()
-    out_b = 30 if f64 else 18            # 3 B texture read + 12|24 B XYZ + 3 B BGR per point
     frame_b = (2 + 2 * (NC + NR)) * H * W
-    total_pts, bytes_alg = 0, 0.0
-    for v in range(Wm, Wm + K):
-        total_pts += pts[v % P]
-        bytes_alg += frame_b + out_b * pts[v % P]
+    out_b = 30 if f64 else 18            # 3 B texture read + 12|24 B XYZ + 3 B BGR per point
 
-    def run_all(batches, events=None):
+    def pool_views(b):
+        return [(b * B + k) % P for k in range(B)]
+
+    total_pts = sum(pts[v] for b in range(Wm, Wm + K) for v in pool_views(b))
+    bytes_alg = sum(frame_b + out_b * pts[v] for b in range(Wm, Wm + K) for v in pool_views(b))
+
+    def run_range(lo, hi, events=None):
         if args.pipeline in ("overlap", "fused"):
-            beng.run_pipelined(batches, s_main, s_stats, events=events, mode=args.pipeline)
+            beng.run_pipelined(batches, s_main, s_stats, events=events, mode=args.pipeline, start=lo, stop=hi)
         else:
-            for k, pb in enumerate(batches):
-                beng.run(pb, events=None if events is None else events[k], stream=s_main)
+            for k in range(lo, hi):
+                beng.run(batches[k], events=None if events is None else events[k - lo], stream=s_main)
 
-    if warm:
-        run_all(warm)
+    # cold start: the priming stats passes + the first launch, alone (not part of the metric)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run_range(0, min(1, Wm))
+    torch.cuda.synchronize()
+    cold_ms = (time.perf_counter() - t0) * 1e3
+    run_range(min(1, Wm), Wm)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_all(timed, events=[(a.cuda_event, b.cuda_event) for a, b in ev])
+    run_range(Wm, Wm + K, events=[(a.cuda_event, b.cuda_event) for a, b in ev])
     t_enq = time.perf_counter() - t0              # host time to enqueue the K steps
     torch.cuda.synchronize()
     if world > 1:
@@ -206,9 +274,40 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in ev)
-    n_launch = len(ev)
     helper_runs = sum(int(np.frombuffer(beng.header(s, k)[3084:3088].cpu().numpy().tobytes(), np.uint32)[0] & 2 != 0)
                       for s in range(2) for k in range(B))
+
+    # ---- verification, outside the timed region: the last timed batch's clouds (nothing wrote
+    # its slot after it) against the plain batch path (bitwise) and one view against the oracle
+    verify = None
+    if not args.no_verify:
+        last = Wm + K - 1
+        slot = last % 2
+        got = [(int(c.count.item()), c.xyz[: int(c.count.item())].clone(), c.bgr[: int(c.count.item())].clone())
+               for c in clouds[slot]]
+        ref_b = prep(last * B, slot)
+        beng.stats(ref_b, stream=s_main)
+        beng.main(ref_b, stream=s_main)
+        s_main.synchronize()
+        same = all(g[0] == int(c.count.item()) and torch.equal(g[1], c.xyz[: g[0]]) and torch.equal(g[2], c.bgr[: g[0]])
+                   for g, c in zip(got, clouds[slot]))
+        counts_ok = [g[0] for g in got] == [pts[v] for v in pool_views(last)]
+        from oracle import sl_oracle as O
+        v0 = pool_views(last)[0]
+        vw = views[v0 % len(views)]
+        oc, orow, om = O.decode_processing(list(vw.frames), n_cols=PW, n_rows=PH, n_sets_col=NC, n_sets_row=NR)
+        Po, Co = O.reconstruct_processing(oc, orow, om, vw.texture, cal, row_mode=1)
+        xg = got[0][1].double().cpu().numpy()
+        rel = float(np.max(np.abs(xg - Po) / np.maximum(np.abs(Po), 1e-3))) if len(Po) == len(xg) else None
+        oracle_ok = (len(Po) == got[0][0] and np.array_equal(got[0][2].cpu().numpy(), Co)
+                     and rel is not None and rel <= (0.0 if f64 else 1e-4))
+        checksum = float(sum(g[1].double().sum().item() for g in got))
+        verify = {"batch": last, "views": B, "pipelined_equals_plain_bitwise": bool(same),
+                  "counts_equal_reference_pass": bool(counts_ok), "oracle_view": int(v0),
+                  "oracle_count_and_colours_equal": bool(len(Po) == got[0][0]), "oracle_xyz_max_rel": rel,
+                  "oracle_ok": bool(oracle_ok), "xyz_checksum": checksum}
+        if not (same and counts_ok and oracle_ok):
+            log(f"[rank {rank}] VERIFY FAILED: {verify}")
 
     stats = torch.tensor([dt, float(total_pts), kern_ms, bytes_alg], dtype=torch.float64, device=dev)
     if world > 1:
@@ -222,21 +321,19 @@ def main():
         dt_max, all_pts, kern_sum, bytes_sum = dt, float(total_pts), kern_ms, bytes_alg
 
     if rank == 0:
-        launches = n_launch * world
+        launches = K * world
         kern_avg_s = kern_sum / launches / 1e3
         achieved = bytes_sum / launches / kern_avg_s / 1e9
+        traffic_view = load_traffic_per_view() if args.config == "c2" else None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                # committed PMC bytes are per C2 view: other workloads report none
-                "traffic": (round(load_traffic_per_view() * K / n_launch)
-                            if load_traffic_per_view() and args.config == "c2" else None),
-                "kernel": "main3_kernel<1,0,1,1> (fused decode+triangulate+compaction, "
-                          f"{B} views per launch)",
+                # committed PMC bytes (profiles/pmc_main_kernel.json) are per C2 view
+                "traffic": round(traffic_view * B) if traffic_view else None,
+                "traffic_source": "profiles/pmc_main_kernel.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"
+                if traffic_view else None,
+                "kernel": f"main3_kernel<1,{int(f64)},1,1> (fused decode+triangulate+compaction, {B} views per launch)",
                 "kernel_avg_us": round(kern_avg_s * 1e6, 2),
                 "alg_bytes_per_launch": round(bytes_sum / launches)}
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(views, cal, args.cpu_seconds, wl)
         out = {
             "metric": METRIC,
             "value": round(all_pts / dt_max / 1e6, 2),
@@ -251,9 +348,11 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": f"{wl['text']}, Otsu, row_mode 1 tol 2.0, XYZ {args.xyz} + BGR out",
+                       "step": f"one batch of {B} views: one fused launch + its thresholds (steady-state pipeline)",
+                       "us_per_view": round(dt_max / (K * B) * 1e6, 3),
+                       "cold_start_ms": round(cold_ms, 3),
                        "views_per_rank": len(views), "device_pool": P, "points_per_view": int(np.mean(pts)),
                        "batch_views": B,
-                       "launches": n_launch,
                        "stats_pipeline": args.pipeline,
                        "lookback_helper_runs": helper_runs,
                        "host_enqueue_ms_per_step": round(t_enq / K * 1e3, 4),
@@ -261,6 +360,7 @@ def main():
                        "parallelism": f"view-sharded x{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "verify": verify,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

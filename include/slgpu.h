@@ -224,6 +224,29 @@ int32_t slg_png_gray8_size(const char *path, int32_t *width, int32_t *height);
 int32_t slg_png_gray8_decode(const char *path, uint8_t *out, int64_t cap, int32_t width,
                              int32_t height);
 
+/* ---- Multi-GPU: the final point-cloud gather of a view-sharded scan.
+ * Replaces nothing in the reference (its batch loop is serial, server/processing.py:314-334);
+ * it is the one collective of the sharded path: after every rank has reconstructed its block
+ * of turntable views, the clouds move to one rank over RCCL (xGMI), exact sizes only.
+ * RCCL is resolved at run time (the librccl.so.1 already in the process, e.g. torch's).
+ *   1. rank 0: slg_gather_unique_id(id); the caller distributes the 128 bytes (e.g. a
+ *      torch.distributed broadcast);  every rank: slg_gather_init(&comm, n_ranks, rank, id),
+ *      with its HIP device current;
+ *   2. slg_gather_counts: all-gather of n_per_rank int64 counts per rank (device buffers,
+ *      all_counts = [n_ranks][n_per_rank]); the caller reads them to size the root's buffer;
+ *   3. slg_gatherv: rank r's send_bytes land at root's recv + sum(recv_bytes[:r]) (recv and the
+ *      HOST array recv_bytes[n_ranks] are read on the root only); grouped point-to-point;
+ *   4. slg_gather_destroy.  All calls enqueue on `stream` (hipStream_t). */
+#define SLG_GATHER_ID_BYTES 128
+typedef struct slg_gather_comm slg_gather_comm;
+int32_t slg_gather_unique_id(uint8_t *id /* [SLG_GATHER_ID_BYTES] */);
+int32_t slg_gather_init(slg_gather_comm **comm, int32_t n_ranks, int32_t rank, const uint8_t *id);
+int32_t slg_gather_counts(slg_gather_comm *comm, const int64_t *counts, int32_t n_per_rank,
+                          int64_t *all_counts, void *stream);
+int32_t slg_gatherv(slg_gather_comm *comm, const void *send, int64_t send_bytes, void *recv,
+                    const int64_t *recv_bytes, int32_t root, void *stream);
+int32_t slg_gather_destroy(slg_gather_comm *comm);
+
 #ifdef __cplusplus
 }
 #endif

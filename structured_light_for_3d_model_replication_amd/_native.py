@@ -97,7 +97,13 @@ EXPORTS = {
     "slg_png_gray8_size": (c_i32, [ctypes.c_char_p, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
     "slg_png_gray8_decode": (c_i32, [ctypes.c_char_p, c_vp, c_i64, c_i32, c_i32]),
     "slg_rays_match_pinhole": (c_i32, [c_vp, c_i32, c_i32, c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_vp]),
+    "slg_gather_unique_id": (c_i32, [c_vp]),
+    "slg_gather_init": (c_i32, [ctypes.POINTER(c_vp), c_i32, c_i32, c_vp]),
+    "slg_gather_counts": (c_i32, [c_vp, c_vp, c_i32, c_vp, c_vp]),
+    "slg_gatherv": (c_i32, [c_vp, c_vp, c_i64, c_vp, ctypes.POINTER(c_i64), c_i32, c_vp]),
+    "slg_gather_destroy": (c_i32, [c_vp]),
 }
+GATHER_ID_BYTES = 128
 
 
 class NativeError(RuntimeError):

@@ -146,7 +146,6 @@ constexpr int kStatsBlocks = 64;            // stats workgroups per view (at mos
 #define SLG_STATS_OTSU_BLOCKS 64                 // 128: 2.6% and 256: 10% slower bench (slot contention)
 #endif
 constexpr int kStatsBlocksOtsu = SLG_STATS_OTSU_BLOCKS;   // matrix-core Otsu path
-constexpr int kStatsPartBlocks = 16;        // partials mode: workgroups per view
 
 struct StatsParams {
   const uint8_t* white[kMaxBatch];
@@ -160,7 +159,7 @@ struct StatsParams {
   double contrast_val;
   int32_t dbg;             // profiling ablation (SLG_DBG bit 4: skip the Otsu tail)
   int32_t pad2;
-  const uint32_t* parts[kMaxBatch];   // Otsu from per-tile partial histograms (NULL: from frames)
+  const uint32_t* parts[kMaxBatch];   // parts_kernel: per-tile partial histograms of each view
   int64_t n_parts;                    // tiles per view
   int64_t pad_zero;                   // zero pixels counted past n_px (removed from bin 0)
 };
@@ -409,21 +408,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
 
   // hist kinds: otsu -> [0] white, [1] clip(white-black); percentile -> [0] black.
   const bool otsu = p.thresh_mode == SLG_THRESH_OTSU;
-  if (otsu && p.parts[view]) {                 // partials of a fused launch: thread t owns bins 2t, 2t+1
-    const uint32_t* pp = p.parts[view];
-    const int64_t per = (p.n_parts + gridDim.x - 1) / gridDim.x;
-    const int64_t t0 = int64_t(blockIdx.x) * per, t1 = t0 + per < p.n_parts ? t0 + per : p.n_parts;
-    uint32_t a0 = 0, a1 = 0;
-#pragma unroll 8
-    for (int64_t k = t0; k < t1; ++k) {
-      const uint32_t v = pp[k * kPartWords + tid];
-      a0 += v & 0xffffu;
-      a1 += v >> 16;
-    }
-    const int i0 = 2 * tid;                    // [white 0..255 | clip 256..511]
-    sh[(i0 >> 8) * kRow + (i0 & 255)] = a0;
-    sh[(i0 >> 8) * kRow + (i0 & 255) + 1] = a1;
-  } else if (otsu) {                           // matrix-core histograms (mfma_hist_chunk)
+  if (otsu) {                                  // matrix-core histograms (mfma_hist_chunk)
     v4i32 acc_w = {0, 0, 0, 0}, acc_d = {0, 0, 0, 0};
     const int lane = tid & 63;
     const int64_t step = int64_t(gridDim.x) * (kBlock / 64) * kHistChunk;
@@ -537,6 +522,81 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
 }
 
+// Otsu thresholds from the per-tile partial histograms a fused launch left in each view's
+// workspace slice (the carried "batch after next", hist_next_*): the lean counterpart of
+// stats_kernel for the streaming pipeline.  It runs on a side stream BESIDE a fused launch, so
+// it holds as few CU resources as it can: 2 KB of LDS, no frame reads, every partial of a
+// workgroup's tile range in flight at once (kPartsInFlight loads per lane), then <= 512 global
+// adds, a ticket, and the same Otsu tail as stats_kernel in the last arriver.
+constexpr int kPartsInFlight = 16;
+constexpr int kPartsBlocksMax = 64;         // workgroups per view (each sums a contiguous tile range)
+
+__global__ __launch_bounds__(kBlock) void parts_kernel(StatsParams p) {
+  __shared__ uint32_t hg[512];
+  __shared__ uint32_t s_last;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const int view = blockIdx.y;
+  WsHeader* ws = p.wsv[view];
+  uint32_t* hist_part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + kHistPartOff);
+  uint64_t* states = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + states_off(p.n_px));
+  const uint32_t* pp = p.parts[view];
+
+  // Arm the compaction state of the following main launch (ordered by the kernel boundary).
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + tid; i < p.n_state_words; i += int64_t(gridDim.x) * kBlock)
+    states[i] = 0;
+  if (blockIdx.x == 0 && tid == 0) ws->tile_counter = 0;
+
+  // thread t owns packed word t (bins 2t, 2t+1 of [white 0..255 | clip 256..511])
+  const int64_t per = (p.n_parts + gridDim.x - 1) / gridDim.x;
+  const int64_t t0 = int64_t(blockIdx.x) * per, t1 = t0 + per < p.n_parts ? t0 + per : p.n_parts;
+  uint32_t a0 = 0, a1 = 0;
+  for (int64_t k0 = t0; k0 < t1; k0 += kPartsInFlight) {
+    uint32_t v[kPartsInFlight];
+#pragma unroll
+    for (int j = 0; j < kPartsInFlight; ++j)
+      v[j] = k0 + j < t1 ? pp[(k0 + j) * kPartWords + tid] : 0u;
+#pragma unroll
+    for (int j = 0; j < kPartsInFlight; ++j) { a0 += v[j] & 0xffffu; a1 += v[j] >> 16; }
+  }
+  uint32_t* dst = hist_part + (blockIdx.x % kHistCopies) * 512 + 2 * tid;
+  if (a0) atomicAdd(dst, a0);
+  if (a1) atomicAdd(dst + 1, a1);
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(&ws->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == gridDim.x - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int i = tid; i < 512; i += kBlock) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int c = 0; c < kHistCopies; ++c)
+      acc += __hip_atomic_load(hist_part + c * 512 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((i & 255) == 0) acc -= uint32_t(p.pad_zero);   // zero padding past n_px
+    hg[i] = acc;
+  }
+  __syncthreads();
+  if (wave < 2) {                              // wave 0: white, wave 1: clip(w-b); concurrently
+    const double thr = otsu_wave(hg + 256 * wave, p.n_px);
+    if ((tid & 63) == 0) {
+      const int m = int_threshold(thr, wave == 0 ? 0 : -255);
+      if (wave == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
+    }
+  }
+  for (int i = tid; i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
+  if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
+}
+
 // ------------------------------------------------------------------ main kernel
 struct MainParams {
   // frames source
@@ -578,9 +638,11 @@ struct MainParams {
   int64_t n_tiles;
   void* scratch_xyz;       // row_mode 2 row cloud
   uint8_t* scratch_bgr;
-  int32_t dbg;             // env SLG_DBG, 0 in production.  Profiling ablations: bit0 no look-back
-                           // wait, bit1 trivial triangulation, bit2 no output stores; test hook:
-                           // bit5 look-back helps unpublished predecessors immediately
+  int32_t dbg;             // env SLG_DBG; read only by the profiling instance (PROF): bit0 no
+                           // look-back wait, bit1 trivial triangulation, bit2 no output stores,
+                           // bit6 per-workgroup phase records, bits 8-15 look-back back-off cap
+  uint32_t help_after;     // look-back: s_sleep(2) units before a silent predecessor is helped
+                           // (kHelpAfter; env SLG_HELP_AFTER=0 forces the helper path in tests)
 };
 
 // code of pixel k (0..7) from the packed accumulators
@@ -835,18 +897,19 @@ constexpr unsigned kHelpAfter = 2048;   // s_sleep(2) units (~0.1 ms) before ask
 // dispatch order is not guaranteed): the caller then computes that tile's aggregate itself
 // (tile_keep_count_wave) and retries, so waiting always ends.  Re-polls only the entries
 // newer than the nearest inclusive prefix, with capped back-off.
+template <bool PROF>
 __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int agg, uint64_t& excl_out,
                              int& help_tile, uint32_t& polls, uint32_t& naps) {
   const int lane = threadIdx.x & 63;
-  if (p.dbg & 1) { excl_out = uint64_t(tile) * kTilePx; return true; }   // ablation: no wait
+  if (PROF && (p.dbg & 1)) { excl_out = uint64_t(tile) * kTilePx; return true; }   // ablation: no wait
   if (tile == 0) {
     if (lane == 0) st_state(&st[0], kFlagInc | uint64_t(agg));
     excl_out = 0;
     return true;
   }
   if (lane == 0) st_state(&st[tile], kFlagAgg | uint64_t(agg));   // a helper only ever writes this same value
-  const unsigned nap_cap = (p.dbg >> 8) & 0xff ? (p.dbg >> 8) & 0xff : kNapCap;   // dbg bits 8-15: A/B
-  const unsigned help_after = (p.dbg & 32) ? 0u : kHelpAfter;                       // dbg 32: tests
+  const unsigned nap_cap = PROF && ((p.dbg >> 8) & 0xff) ? (p.dbg >> 8) & 0xff : kNapCap;   // dbg bits 8-15: A/B
+  const unsigned help_after = p.help_after;
   uint64_t excl = 0;
   int64_t j = tile - 1;
   for (;;) {
@@ -947,18 +1010,6 @@ __global__ __launch_bounds__(kBlock) void decode_maps_kernel(MainParams p) {
 constexpr int kMaxViews = 16;
 #ifndef SLG_DECODE_BATCH
 #define SLG_DECODE_BATCH 11                // pairs per axis in flight per lane (4/6/8/11: 31.7/30.3/28.7/27.5 us/view)
-#endif
-#ifndef SLG_VIEW_MAJOR
-#define SLG_VIEW_MAJOR 0                   // 1: all tiles of view 0 first, then view 1, ...
-#endif
-#ifndef SLG_STAGED_STORES
-#define SLG_STAGED_STORES 0                // 1: phase D via LDS-packed contiguous stores (measured 355 vs 347 us per launch)
-#endif
-#ifndef SLG_NT_STORES
-#define SLG_NT_STORES 0                    // A/B: 1 = phase-D cloud stores non-temporal
-#endif
-#ifndef SLG_PRIO
-#define SLG_PRIO 0                         // A/B: 1 = wave priority 2 in phase A, 0 after; 2 = 0 in A, 2 after
 #endif
 #ifndef SLG_M3_WAVES
 #define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
@@ -1101,7 +1152,9 @@ __device__ inline int2 block_scan(int x, int* s_wtot) {
   return make_int2(off + incl - x, tot);
 }
 
-template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS>
+// PROF: the profiling instance (SLG_DBG set): honours the ablation bits of MainParams::dbg and
+// writes per-workgroup phase records; the production instances carry none of that code.
+template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS, bool PROF>
 __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) void main3_kernel(Main3Params P) {
   using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
   constexpr int NS = ROW_MODE == 2 ? 2 : 1;
@@ -1118,24 +1171,20 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = int(P.c.n_tiles);
-#if SLG_VIEW_MAJOR
-  const int view = int(blockIdx.x) / tiles;          // grid = views x tiles, view-major
-  const int tile = int(blockIdx.x) - view * tiles;
-#else
   // Views interleaved in dispatch order: each view's look-back chain has only ~1/n_views of
   // the resident workgroups in flight, so a tile waits on fewer, similar predecessors.
   const int tile = int(blockIdx.x) / P.n_views;
   const int view = int(blockIdx.x) - tile * P.n_views;
-#endif
   const MainParams p = view_params(P, view);
   const int64_t tile_px = int64_t(tile) * kTilePx;
   const int64_t px0 = tile_px + int64_t(tid) * kPx;
   const bool tail = tile == tiles - 1;               // block-uniform: guarded reads only here
   const int tile_v0 = int(tile_px / p.width);
-  // Profiling (SLG_DBG bit 6): per workgroup one 32-byte record {A decode, B triangulate,
-  // C look-back, D stores (100 MHz ticks), look-back polls, sleep units, items, start} written
-  // to view 0's partials region (tools/kbench.py "phases"; unused unless batches are carried).
-  const bool prof = (p.dbg & 64) != 0;
+  // PROF, SLG_DBG bit 6: per workgroup one 32-byte record {A decode, B triangulate, C
+  // look-back, D stores (100 MHz ticks), look-back polls, sleep units, items, start} written to
+  // view 0's partials region (tools/kbench.py "phases"; the host refuses it when a batch is
+  // carried, whose partials live there).
+  const bool prof = PROF && (p.dbg & 64) != 0;
   uint64_t t_phase = prof ? __builtin_amdgcn_s_memrealtime() : 0;
   uint32_t rec[8] = {0, 0, 0, 0, 0, 0, 0, uint32_t(t_phase)};   // [7]: start time (low 32 bits)
   auto stamp = [&](int k) {
@@ -1154,7 +1203,6 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     for (int i = tid; i < 512; i += kB) s_hn[i] = 0;   // ordered before phase C by block_scan's barrier
   }
   // ------------------------------------------------------------ A: decode + tile compaction
-  if (SLG_PRIO == 1) __builtin_amdgcn_s_setprio(2);
   int n_items;
   {
     uint32_t tex[6] = {0, 0, 0, 0, 0, 0};
@@ -1186,8 +1234,6 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     }
   }
   __syncthreads();
-  if (SLG_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-  if (SLG_PRIO == 2) __builtin_amdgcn_s_setprio(2);
 
   stamp(0);
   // ------------------------------------------------------------ B: triangulate, balanced
@@ -1197,7 +1243,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   XT pts[NS][kIt][3];
   uint64_t km[NS][kIt];
   static_assert(kIt % 2 == 0, "paired rounds");
-  if (p.rays_fast && !(p.dbg & 2)) {
+  const bool trivial = PROF && (p.dbg & 2);          // ablation: no triangulation arithmetic
+  if (p.rays_fast && !trivial) {
     // Two rounds per step: two independent straight-line fp64 chains (and their plane
     // gathers) per lane, so the latency of one hides behind the other.
 #pragma unroll
@@ -1233,34 +1280,34 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     }
   } else {
 #pragma unroll
-  for (int i = 0; i < kIt; ++i) {
+    for (int i = 0; i < kIt; ++i) {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) km[s][i] = 0;
-    if (i * kB < n_items) {                          // block-uniform
-      const int m = tid + kB * i;
-      const bool in = m < n_items;
-      const uint32_t sc = s_code[m], suv = s_uv[m];   // read unconditionally (m < kTilePx) ...
-      const uint32_t code = in ? sc : 0u, uv = in ? suv : 0u;   // ... garbage past n_items masked
-      const int u = int(uv & 0xffffu), v = int(uv >> 16);
-      uint32_t keep;
-      if (p.dbg & 2) {                               // ablation: trivial triangulation
-        keep = in ? (ROW_MODE == 2 ? 3u : 1u) : 0u;
-        pts[0][i][0] = XT(code & 0xffff); pts[0][i][1] = XT(code >> 16); pts[0][i][2] = XT(u);
-        if constexpr (ROW_MODE == 2) { pts[NS - 1][i][0] = XT(v); pts[NS - 1][i][1] = 0; pts[NS - 1][i][2] = 0; }
-      } else {
-        const TriOut o = tri_item<ROW_MODE, RAYS>(p, code, u, v);
-        keep = in ? o.keep : 0u;
-        pts[0][i][0] = XT(o.x); pts[0][i][1] = XT(o.y); pts[0][i][2] = XT(o.z);
-        if constexpr (ROW_MODE == 2) { pts[NS - 1][i][0] = XT(o.rx); pts[NS - 1][i][1] = XT(o.ry); pts[NS - 1][i][2] = XT(o.rz); }
+      for (int s = 0; s < NS; ++s) km[s][i] = 0;
+      if (i * kB < n_items) {                          // block-uniform
+        const int m = tid + kB * i;
+        const bool in = m < n_items;
+        const uint32_t sc = s_code[m], suv = s_uv[m];   // read unconditionally (m < kTilePx) ...
+        const uint32_t code = in ? sc : 0u, uv = in ? suv : 0u;   // ... garbage past n_items masked
+        const int u = int(uv & 0xffffu), v = int(uv >> 16);
+        uint32_t keep;
+        if (trivial) {
+          keep = in ? (ROW_MODE == 2 ? 3u : 1u) : 0u;
+          pts[0][i][0] = XT(code & 0xffff); pts[0][i][1] = XT(code >> 16); pts[0][i][2] = XT(u);
+          if constexpr (ROW_MODE == 2) { pts[NS - 1][i][0] = XT(v); pts[NS - 1][i][1] = 0; pts[NS - 1][i][2] = 0; }
+        } else {
+          const TriOut o = tri_item<ROW_MODE, RAYS>(p, code, u, v);
+          keep = in ? o.keep : 0u;
+          pts[0][i][0] = XT(o.x); pts[0][i][1] = XT(o.y); pts[0][i][2] = XT(o.z);
+          if constexpr (ROW_MODE == 2) { pts[NS - 1][i][0] = XT(o.rx); pts[NS - 1][i][1] = XT(o.ry); pts[NS - 1][i][2] = XT(o.rz); }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) km[s][i] = __ballot((keep >> s) & 1u);
       }
+      if (lane == 0) {
 #pragma unroll
-      for (int s = 0; s < NS; ++s) km[s][i] = __ballot((keep >> s) & 1u);
+        for (int s = 0; s < NS; ++s) s_cnt[s][i][wave] = __popcll(km[s][i]);
+      }
     }
-    if (lane == 0) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) s_cnt[s][i][wave] = __popcll(km[s][i]);
-    }
-  }
   }
   if (hn) hist_next_stage(hn_w, hn_b, p.n_px, px0, s_hstage);
   __syncthreads();
@@ -1275,7 +1322,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       uint64_t* st = p.states + int64_t(s) * tiles;
       uint64_t excl;
       int ht;
-      while (!lookback_try(p, st, tile, agg, excl, ht, rec[4], rec[5])) {
+      while (!lookback_try<PROF>(p, st, tile, agg, excl, ht, rec[4], rec[5])) {
         // a predecessor has not published for long (it may not be dispatched yet): publish
         // its aggregate for it, computed by this wave, and look back again
         const int hagg = tile_keep_count_wave<ROW_MODE, SRC_FRAMES, RAYS>(p, ht, s);
@@ -1300,51 +1347,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
 
   stamp(2);
   // ------------------------------------------------------------ D: ordered stores from registers
-  if (p.dbg & 4) return;                             // ablation: no output stores
+  if (PROF && (p.dbg & 4)) return;                   // ablation: no output stores
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-#if SLG_STAGED_STORES
-  // Per wave and round, the kept points are packed in LDS (s_code / s_uv are dead after phase
-  // B) and written back as contiguous elements: each store instruction covers 256 B (f32) of
-  // one run of the cloud instead of a 12-byte-strided scatter, and the BGR bytes likewise.
-  static_assert(4 * 64 * 3 * sizeof(XT) <= sizeof(s_code) && 4 * 64 * 3 <= sizeof(s_uv), "staging");
-  XT* stg = reinterpret_cast<XT*>(s_code) + wave * (64 * 3);
-  uint8_t* stb = reinterpret_cast<uint8_t*>(s_uv) + wave * (64 * 3);
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    int64_t base = int64_t(s_excl[s]);
-    XT* gx = reinterpret_cast<XT*>(s == 0 ? p.xyz : p.scratch_xyz);
-    uint8_t* gb = s == 0 ? p.bgr : p.scratch_bgr;
-#pragma unroll
-    for (int i = 0; i < kIt; ++i) {
-      int before = 0, round = 0;
-#pragma unroll
-      for (int w = 0; w < kB / 64; ++w) {
-        const int c = s_cnt[s][i][w];
-        before += w < wave ? c : 0;
-        round += c;
-      }
-      const int n3 = 3 * __popcll(km[s][i]);        // wave-uniform
-      if (n3) {
-        if ((km[s][i] >> lane) & 1ull) {
-          const int r = 3 * __popcll(km[s][i] & lt);
-          stg[r] = pts[s][i][0]; stg[r + 1] = pts[s][i][1]; stg[r + 2] = pts[s][i][2];
-          const uint32_t c = s_bgr[tid + kB * i];
-          stb[r] = uint8_t(c); stb[r + 1] = uint8_t(c >> 8); stb[r + 2] = uint8_t(c >> 16);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int64_t q3 = 3 * (base + before);
-        for (int j = lane; j < n3; j += 64) gx[q3 + j] = stg[j];
-        for (int j = lane; j < n3; j += 64) gb[q3 + j] = stb[j];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // reads done before the next round's writes
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-      base += round;
-    }
-  }
-#else
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     int64_t base = int64_t(s_excl[s]);
@@ -1362,22 +1366,12 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       if ((km[s][i] >> lane) & 1ull) {
         const int64_t q = base + before + __popcll(km[s][i] & lt);
         const uint32_t c = s_bgr[tid + kB * i];
-        if (SLG_NT_STORES) {
-          __builtin_nontemporal_store(pts[s][i][0], &gx[3 * q]);
-          __builtin_nontemporal_store(pts[s][i][1], &gx[3 * q + 1]);
-          __builtin_nontemporal_store(pts[s][i][2], &gx[3 * q + 2]);
-          __builtin_nontemporal_store(uint8_t(c), &gb[3 * q]);
-          __builtin_nontemporal_store(uint8_t(c >> 8), &gb[3 * q + 1]);
-          __builtin_nontemporal_store(uint8_t(c >> 16), &gb[3 * q + 2]);
-        } else {
-          gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
-          gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
-        }
+        gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
+        gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
       }
       base += round;
     }
   }
-#endif
   if (prof) {
     __syncthreads();
     stamp(3);
@@ -1540,7 +1534,12 @@ int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* black
     const int64_t need = (n_px + per_block - 1) / per_block;
     if (grid < need) grid = need;
   }
-  if (from_parts) grid = sp.n_parts < kStatsPartBlocks ? sp.n_parts : kStatsPartBlocks;
+  if (from_parts) {   // ~2 x kPartsInFlight tiles per workgroup: one or two rounds of loads
+    grid = (sp.n_parts + 2 * kPartsInFlight - 1) / (2 * kPartsInFlight);
+    grid = grid < 1 ? 1 : (grid > kPartsBlocksMax ? kPartsBlocksMax : grid);
+    hipLaunchKernelGGL(parts_kernel, dim3(unsigned(grid), unsigned(n_views)), dim3(kBlock), 0, s, sp);
+    return check_launch("parts_kernel");
+  }
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(stats_kernel, dim3(unsigned(grid), unsigned(n_views)), dim3(kBlock), 0, s, sp);
   return check_launch("stats_kernel");
@@ -1612,11 +1611,23 @@ int debug_flags() {   // profiling ablations only; unset in production
   return e ? atoi(e) : 0;
 }
 
+constexpr int kMainDbgBits = 1 | 2 | 4 | 64 | 0xff00;   // bits main3's profiling instance reads
+
+uint32_t help_after() {   // look-back helper delay; SLG_HELP_AFTER=0 forces the helper (tests)
+  const char* e = getenv("SLG_HELP_AFTER");
+  return e ? uint32_t(atoi(e)) : kHelpAfter;
+}
+
 using Main3Fn = void (*)(Main3Params);
 
+// Production instances for every (row_mode, xyz, source, ray) case; the profiling instance
+// (SLG_DBG with any main3 bit) exists for the benchmark shape only: row_mode 1, f32 XYZ, frames,
+// pinhole rays (tools/kbench.py).
 template <int SRC>
 Main3Fn pick_main(int row_mode, int x64, int rays) {
-#define SLG_CASE(RM, X, R) if (row_mode == RM && x64 == X && rays == R) return main3_kernel<RM, X, SRC, R>;
+  if (debug_flags() & kMainDbgBits)
+    return (SRC == 1 && row_mode == 1 && x64 == 0 && rays == SLG_RAYS_PINHOLE) ? main3_kernel<1, 0, 1, 1, true> : nullptr;
+#define SLG_CASE(RM, X, R) if (row_mode == RM && x64 == X && rays == R) return main3_kernel<RM, X, SRC, R, false>;
   SLG_CASE(0, 0, 0) SLG_CASE(0, 0, 1) SLG_CASE(0, 1, 0) SLG_CASE(0, 1, 1)
   SLG_CASE(1, 0, 0) SLG_CASE(1, 0, 1) SLG_CASE(1, 1, 0) SLG_CASE(1, 1, 1)
   SLG_CASE(2, 0, 0) SLG_CASE(2, 0, 1) SLG_CASE(2, 1, 0) SLG_CASE(2, 1, 1)
@@ -1636,8 +1647,10 @@ int fill_view(ViewIO& io, const slg_cloud* out, const slg_tri_params* tp, int64_
 
 // One main3 launch over mp.n_views views (<= kMaxViews), then the row_mode-2 tails.
 int launch_main3(Main3Fn fn, Main3Params& mp, const slg_tri_params* tp, const slg_cloud* outs, hipStream_t s) {
-  if (!fn) return fail(SLG_ERR_INVALID, "no kernel for this configuration");
+  if (!fn) return fail(SLG_ERR_UNSUPPORTED, "no kernel for this configuration (SLG_DBG profiling: "
+                                            "row_mode 1, f32, frames, pinhole only)");
   mp.c.dbg = debug_flags();
+  mp.c.help_after = help_after();
   const int64_t grid = mp.c.n_tiles * mp.n_views;
   if (grid > INT_MAX) return fail(SLG_ERR_UNSUPPORTED, "batch too large for one launch");
   hipLaunchKernelGGL(fn, dim3(unsigned(grid)), dim3(kTileBlock), 0, s, mp);
@@ -1680,6 +1693,8 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
   if (n_next) {                                     // the batch after next rides along (Otsu only)
     if (!next || n_next < 0 || n_next > n_views) return fail(SLG_ERR_INVALID, "next batch: NULL or more views than this batch");
     if (dp->thresh_mode != SLG_THRESH_OTSU) return fail(SLG_ERR_UNSUPPORTED, "next-batch histograms need thresh_mode OTSU");
+    if (debug_flags() & 64)   // the phase records would land on the carried partials
+      return fail(SLG_ERR_UNSUPPORTED, "SLG_DBG phase records cannot run with a carried batch");
     for (int v = 0; v < n_next; ++v) {
       rc = check_capture(&next[v]);
       if (rc) return rc;
@@ -1722,10 +1737,10 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
         io.hn_part = reinterpret_cast<uint32_t*>(ws + int64_t(v) * ws_stride + parts_off(n_px));
       }
     }
-    if (timing_events && timing_events[2 * launch]) hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * launch]), s);
+    if (timing_events && timing_events[2 * launch]) (void)hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * launch]), s);
     rc = launch_main3(fn, mp, tp, &outs[v0], s);
     if (rc) return rc;
-    if (timing_events && timing_events[2 * launch + 1]) hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * launch + 1]), s);
+    if (timing_events && timing_events[2 * launch + 1]) (void)hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * launch + 1]), s);
   }
   return SLG_OK;
 }
@@ -1819,6 +1834,15 @@ char* fmt_u8(unsigned v, char* p) {
 }
 
 }  // namespace
+
+// Error entry for the library's other translation units (csrc/gather.cpp).
+int slg_internal_fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
 
 // ==================================================================== C ABI
 extern "C" {

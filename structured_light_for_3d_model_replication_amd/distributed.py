@@ -8,9 +8,10 @@ data path.  Two optional collectives exist for the end of a job:
 
 * ``batch_summary`` — all-reduce of per-rank success counts so rank 0 can log the reference's
   ``=== Batch Complete: s/n succeeded ===`` line for the whole job;
-* ``gather_clouds`` — gatherv of the per-view clouds to rank 0 (counts first, then padded
-  XYZ/BGR buffers) over RCCL/xGMI (backend ``nccl``) or gloo, for a consumer that wants
-  every point on one rank (e.g. the 360° merge that follows the path).
+* ``RcclCloudGather`` — the final cloud gather of the north star: exact-size gatherv of the
+  per-view clouds to rank 0 through the C ABI over RCCL/xGMI (``slg_gather_*``), for a
+  consumer that wants every point on one rank (e.g. the 360° merge that follows the path);
+  ``gather_clouds`` is the same protocol over torch.distributed (gloo or RCCL).
 """
 from __future__ import annotations
 
@@ -54,9 +55,12 @@ def batch_summary(success: int, total: int, device=None) -> tuple[int, int]:
 
 
 def gather_clouds(xyz: torch.Tensor, bgr: torch.Tensor, dst: int = 0):
-    """Gatherv of variable-size clouds to ``dst``: returns ``[(xyz_r, bgr_r), ...]`` on ``dst``
-    (rank order), ``None`` elsewhere.  ``xyz`` [n,3] float, ``bgr`` [n,3] uint8, same device
-    as the process group's backend expects (CUDA for RCCL, CPU for gloo)."""
+    """Exact-size gatherv of variable-size clouds to ``dst`` over torch.distributed (gloo or
+    RCCL): the counts go by one all_gather, then every rank sends exactly its own points
+    (point-to-point, grouped; no padding to the largest rank).  Returns ``[(xyz_r, bgr_r), ...]``
+    on ``dst`` (rank order), ``None`` elsewhere.  ``xyz`` [n,3] float, ``bgr`` [n,3] uint8, on the
+    device the process group's backend expects (CUDA for RCCL, CPU for gloo).  The C-ABI RCCL
+    path for GPU clouds is :class:`RcclCloudGather`."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return [(xyz, bgr)]
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -64,18 +68,110 @@ def gather_clouds(xyz: torch.Tensor, bgr: torch.Tensor, dst: int = 0):
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n)
     counts = [int(c.item()) for c in counts]
-    cap = max(max(counts), 1)
-    px = torch.zeros((cap, 3), dtype=xyz.dtype, device=xyz.device)
-    pb = torch.zeros((cap, 3), dtype=torch.uint8, device=xyz.device)
-    px[: xyz.shape[0]] = xyz
-    pb[: xyz.shape[0]] = bgr
-    gx = [torch.empty_like(px) for _ in range(world)] if rank == dst else None
-    gb = [torch.empty_like(pb) for _ in range(world)] if rank == dst else None
-    dist.gather(px, gx, dst=dst)
-    dist.gather(pb, gb, dst=dst)
-    if rank != dst:
-        return None
-    return [(x[:c], b[:c]) for c, x, b in zip(counts, gx, gb)]
+    nccl = dist.get_backend() == "nccl"
+    ops, reqs = [], []
+
+    def p2p(fn, t, peer):
+        if nccl:
+            ops.append(dist.P2POp(fn, t, peer))
+        else:
+            reqs.append(fn(t, peer))
+
+    out = None
+    if rank == dst:
+        out = []
+        for r in range(world):
+            if r == dst:
+                out.append((xyz, bgr))
+                continue
+            bx = torch.empty((counts[r], 3), dtype=xyz.dtype, device=xyz.device)
+            bb = torch.empty((counts[r], 3), dtype=torch.uint8, device=xyz.device)
+            if counts[r]:
+                p2p(dist.irecv, bx, r)
+                p2p(dist.irecv, bb, r)
+            out.append((bx, bb))
+    elif counts[rank]:
+        p2p(dist.isend, xyz.contiguous(), dst)
+        p2p(dist.isend, bgr.contiguous(), dst)
+    if ops:
+        reqs += dist.batch_isend_irecv(ops)
+    for q in reqs:
+        q.wait()
+    return out
+
+
+class RcclCloudGather:
+    """The final cloud gather through the C ABI (``slg_gather_*`` over the process's RCCL):
+    one communicator per job (its 128-byte id travels by a torch.distributed broadcast), then
+    per gather one all-gather of the per-view counts and one grouped exact-size gatherv of XYZ
+    and of BGR to the root.  Every rank calls :meth:`gather` with its block of views."""
+
+    def __init__(self, device=None):
+        import ctypes
+        from . import _native as N
+        self.N, self.ct = N, ctypes
+        pg = dist.is_available() and dist.is_initialized()
+        self.rank, self.world = (dist.get_rank(), dist.get_world_size()) if pg else (0, 1)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        uid = torch.zeros(N.GATHER_ID_BYTES, dtype=torch.uint8)
+        if self.rank == 0:
+            N.check(N.lib().slg_gather_unique_id(ctypes.c_void_p(uid.data_ptr())))
+        if not pg:
+            pass
+        elif dist.get_backend() == "nccl":
+            d = uid.to(self.device)
+            dist.broadcast(d, 0)
+            uid = d.cpu()
+        else:
+            dist.broadcast(uid, 0)
+        self._uid = uid
+        self.comm = ctypes.c_void_p()
+        N.check(N.lib().slg_gather_init(ctypes.byref(self.comm), self.world, self.rank,
+                                        ctypes.c_void_p(uid.data_ptr())))
+
+    def close(self):
+        if self.comm:
+            self.N.check(self.N.lib().slg_gather_destroy(self.comm))
+            self.comm = self.ct.c_void_p()
+
+    def gather(self, clouds, n_per_rank: int, root: int = 0, stream=None):
+        """``clouds``: this rank's ``[(xyz [n,3], bgr [n,3] uint8), ...]`` (device tensors, at most
+        ``n_per_rank`` views).  Returns on ``root`` the list over every rank's views (rank-major)
+        of ``(xyz, bgr)`` slices of one gathered device buffer; ``None`` elsewhere."""
+        N, ct = self.N, self.ct
+        if len(clouds) > n_per_rank:
+            raise ValueError("more views than n_per_rank")
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        sp = ct.c_void_p(s.cuda_stream)
+        dt = clouds[0][0].dtype if clouds else torch.float32
+        with torch.cuda.stream(s):
+            cnt = torch.zeros(n_per_rank, dtype=torch.int64, device=self.device)
+            for k, (x, _) in enumerate(clouds):
+                cnt[k] = x.shape[0]
+            allc = torch.empty(self.world * n_per_rank, dtype=torch.int64, device=self.device)
+            N.check(N.lib().slg_gather_counts(self.comm, ct.c_void_p(cnt.data_ptr()), n_per_rank,
+                                              ct.c_void_p(allc.data_ptr()), sp))
+            counts = allc.cpu().tolist()                  # sizes the root's buffers (host sync)
+            xs = torch.cat([x.reshape(-1, 3) for x, _ in clouds]) if clouds else torch.empty((0, 3), dtype=dt, device=self.device)
+            bs = torch.cat([b.reshape(-1, 3) for _, b in clouds]) if clouds else torch.empty((0, 3), dtype=torch.uint8, device=self.device)
+            per_rank = [sum(counts[r * n_per_rank:(r + 1) * n_per_rank]) for r in range(self.world)]
+            total = sum(per_rank)
+            esz = xs.element_size() * 3
+            rx = torch.empty((total, 3), dtype=dt, device=self.device) if self.rank == root else None
+            rb = torch.empty((total, 3), dtype=torch.uint8, device=self.device) if self.rank == root else None
+            for send, recv, width in ((xs, rx, esz), (bs, rb, 3)):
+                rbytes = (ct.c_int64 * self.world)(*[c * width for c in per_rank])
+                N.check(N.lib().slg_gatherv(self.comm, ct.c_void_p(send.data_ptr()), send.shape[0] * width,
+                                            ct.c_void_p(recv.data_ptr() if recv is not None else 0),
+                                            rbytes, root, sp))
+        self.last_buffers = (rx, rb)                      # root: the gathered job, contiguous
+        if self.rank != root:
+            return None
+        out, off = [], 0
+        for c in counts:
+            out.append((rx[off:off + c], rb[off:off + c]))
+            off += c
+        return out
 
 
 def process_batch_sharded(calib_path, target_path, log_callback=None, process_source=None, **kw):

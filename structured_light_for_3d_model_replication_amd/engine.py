@@ -189,14 +189,24 @@ class Cloud:
         self.bgr = torch.empty((self.capacity, 3), device=device, dtype=torch.uint8)
         self.count = torch.zeros(1, device=device, dtype=torch.int64)
         self.xyz_f64 = xyz_f64
+        self.stream = None            # stream of the last launch that wrote this cloud
 
     def struct(self) -> N.Cloud:
         return N.Cloud(xyz=self.xyz.data_ptr(), bgr=self.bgr.data_ptr(),
                        count=self.count.data_ptr(), capacity=self.capacity)
 
     def result(self):
+        """``(xyz[:n], bgr[:n])`` once the launch that wrote this cloud has finished: the
+        current stream first waits for the launch stream, so ``count`` is never read early."""
+        cur = torch.cuda.current_stream(self.count.device)
+        if self.stream is not None and self.stream != cur:
+            cur.wait_stream(self.stream)
         n = int(self.count.item())
         return self.xyz[:n], self.bgr[:n]
+
+    def _launched_on(self, stream):
+        self.stream = stream if stream is not None else torch.cuda.current_stream(self.count.device)
+        return self
 
 
 class Reconstructor:
@@ -238,7 +248,7 @@ class Reconstructor:
         c, tp, o = calib.struct(), N.TriParams(int(row_mode), int(out.xyz_f64), float(epipolar_tol)), out.struct()
         N.check(N.lib().slg_triangulate(ctypes.byref(maps), ctypes.byref(c), ctypes.byref(tp),
                                         _vp(self.workspace), ctypes.byref(o), _stream(stream)))
-        return out
+        return out._launched_on(stream)
 
     def reconstruct(self, frames: DeviceFrames, cfg: DecodeConfig, calib: DeviceCalib, row_mode=1,
                     epipolar_tol=2.0, xyz_f64=True, out: Cloud | None = None, stream=None):
@@ -251,7 +261,7 @@ class Reconstructor:
         N.check(N.lib().slg_reconstruct(ctypes.byref(cap), ctypes.byref(dp), ctypes.byref(c),
                                         ctypes.byref(tp), _vp(self.workspace), ctypes.byref(o),
                                         _stream(stream)))
-        return out
+        return out._launched_on(stream)
 
     def stats(self, frames: DeviceFrames, cfg: DecodeConfig, stream=None):
         """Mask-threshold pass alone (``slg_decode_stats``); arms the workspace."""
@@ -269,6 +279,7 @@ class Reconstructor:
         N.check(N.lib().slg_decode_triangulate(ctypes.byref(cap), ctypes.byref(dp), ctypes.byref(c),
                                                ctypes.byref(tp), _vp(self.workspace),
                                                ctypes.byref(o), _stream(stream)))
+        out._launched_on(stream)
 
     def launch_structs(self, frames, cfg, calib, out, row_mode=1, epipolar_tol=2.0):
         """Pre-built ctypes argument structs (lets a hot loop skip their construction)."""
@@ -299,6 +310,11 @@ class PreparedBatch:
     tp: object
     clouds: object
     slot: int
+    outs: list = None             # the Cloud objects behind ``clouds``
+
+    def launched_on(self, stream):
+        for o in self.outs or ():
+            o._launched_on(stream)
 
     @property
     def n_launches(self) -> int:
@@ -349,7 +365,7 @@ class BatchReconstructor:
         clouds = (N.Cloud * n)(*[o.struct() for o in outs])
         return PreparedBatch(caps, n, cfg.struct(), calib.struct(),
                              N.TriParams(int(row_mode), int(outs[0].xyz_f64), float(epipolar_tol)),
-                             clouds, slot)
+                             clouds, slot, list(outs))
 
     @staticmethod
     def _events_arg(pb: PreparedBatch, events):
@@ -363,6 +379,7 @@ class BatchReconstructor:
         N.check(N.lib().slg_reconstruct_batch(pb.caps, pb.n, ctypes.byref(pb.dp), ctypes.byref(pb.calib),
                                               ctypes.byref(pb.tp), self._ws(pb.slot), self.ws_stride,
                                               pb.clouds, self._events_arg(pb, events), _stream(stream)))
+        pb.launched_on(stream)
 
     def stats(self, pb: PreparedBatch, stream=None):
         N.check(N.lib().slg_decode_stats_batch(pb.caps, pb.n, ctypes.byref(pb.dp), self._ws(pb.slot),
@@ -373,6 +390,7 @@ class BatchReconstructor:
                                                      ctypes.byref(pb.calib), ctypes.byref(pb.tp),
                                                      self._ws(pb.slot), self.ws_stride, pb.clouds,
                                                      self._events_arg(pb, events), _stream(stream)))
+        pb.launched_on(stream)
 
     def main_next(self, pb: PreparedBatch, nxt: PreparedBatch, events=None, stream=None):
         """Fused launch of ``pb`` that also histograms ``nxt`` (the batch after next, same
@@ -382,15 +400,17 @@ class BatchReconstructor:
         N.check(N.lib().slg_decode_triangulate_batch_next(
             pb.caps, pb.n, ctypes.byref(pb.dp), ctypes.byref(pb.calib), ctypes.byref(pb.tp), self._ws(pb.slot),
             self.ws_stride, pb.clouds, nxt.caps, nxt.n, self._events_arg(pb, events), _stream(stream)))
+        pb.launched_on(stream)
 
     def stats_partials(self, pb: PreparedBatch, stream=None):
         """Thresholds of ``pb`` from the partials a fused launch left in its slot."""
         N.check(N.lib().slg_decode_stats_partials_batch(pb.n, self.height, self.width, ctypes.byref(pb.dp),
                                                         self._ws(pb.slot), self.ws_stride, _stream(stream)))
 
-    def run_pipelined(self, batches, main_stream, stats_stream, events=None, mode="fused"):
-        """Run ``batches`` (PreparedBatch list; consecutive ones on different slots) with their
-        stats off the fused launches' critical path.
+    def run_pipelined(self, batches, main_stream, stats_stream, events=None, mode="fused",
+                      start=0, stop=None):
+        """Launch ``batches[start:stop]`` (PreparedBatch list; consecutive ones on different
+        slots) with their stats off the fused launches' critical path.
 
         mode "overlap": the stats pass of batch k+1 runs on ``stats_stream`` beside batch k's
         fused launch on ``main_stream``.
@@ -399,47 +419,61 @@ class BatchReconstructor:
         ``stats_stream`` turns them into thresholds beside batch k+1's launch.  Needs Otsu
         thresholds and slots alternating k % 2; the first two batches (and any batch with more
         views than the one carrying it) get a regular stats pass.
-        ``events[k]``: timing events for batch k's fused launches, or None."""
+
+        The list is a stream: a call with ``start > 0`` continues the pipeline where the call
+        that stopped at ``start`` left it (the thresholds of batches ``start`` and ``start+1``
+        were armed by that call), so a long run can be issued in pieces -- e.g. warmup and timed
+        steps -- without restarting it.  Batches past ``stop`` are only prepared for (their
+        stats / histograms), never launched.  ``events[k - start]``: timing events for batch
+        k's fused launches, or None."""
         n = len(batches)
+        stop = n if stop is None else min(int(stop), n)
+        if not 0 <= start <= stop:
+            raise ValueError("bad start/stop")
         for k in range(1, n):
             if batches[k].slot == batches[k - 1].slot:
                 raise ValueError("consecutive batches must use different workspace slots")
         while len(self._events) < 2 * n:
             self._events.append(torch.cuda.Event())
         st_ev, mn_ev = self._events[0::2], self._events[1::2]
+
+        def ev_of(k):
+            return None if events is None else events[k - start]
+
         if mode == "fused" and n and all(b.dp.thresh_mode == N.THRESH_OTSU for b in batches):
-            for k in range(min(2, n)):
-                self.stats(batches[k], stream=stats_stream)
-                st_ev[k].record(stats_stream)
-            for k in range(n):
+            if start == 0:
+                for k in range(min(2, n)):
+                    self.stats(batches[k], stream=stats_stream)
+                    st_ev[k].record(stats_stream)
+            for k in range(start, stop):
                 nxt = batches[k + 2] if k + 2 < n else None
                 carry = nxt is not None and nxt.slot == batches[k].slot and nxt.n <= batches[k].n
                 main_stream.wait_event(st_ev[k])
-                ev = None if events is None else events[k]
                 if carry:
-                    self.main_next(batches[k], nxt, events=ev, stream=main_stream)
+                    self.main_next(batches[k], nxt, events=ev_of(k), stream=main_stream)
                 else:
-                    self.main(batches[k], events=ev, stream=main_stream)
+                    self.main(batches[k], events=ev_of(k), stream=main_stream)
                 mn_ev[k].record(main_stream)
                 if nxt is not None:                        # batch k+2 reuses batch k's slot
                     stats_stream.wait_event(mn_ev[k])
                     (self.stats_partials if carry else self.stats)(nxt, stream=stats_stream)
                     st_ev[k + 2].record(stats_stream)
-            stats_stream.wait_event(mn_ev[n - 1])
+            if stop > start:
+                stats_stream.wait_event(mn_ev[stop - 1])
             return
         if mode not in ("fused", "overlap"):
             raise ValueError(f"unknown pipeline mode {mode!r}")
-        if n:
+        if n and start == 0:
             self.stats(batches[0], stream=stats_stream)
             st_ev[0].record(stats_stream)
-        for k in range(n):
+        for k in range(start, stop):
             if k + 1 < n:
                 if k >= 1:                                 # batch k+1 reuses batch k-1's slot
                     stats_stream.wait_event(mn_ev[k - 1])
                 self.stats(batches[k + 1], stream=stats_stream)
                 st_ev[k + 1].record(stats_stream)
             main_stream.wait_event(st_ev[k])
-            self.main(batches[k], events=None if events is None else events[k], stream=main_stream)
+            self.main(batches[k], events=ev_of(k), stream=main_stream)
             mn_ev[k].record(main_stream)
-        if n:
-            stats_stream.wait_event(mn_ev[n - 1])          # callers may sync either stream
+        if stop > start:
+            stats_stream.wait_event(mn_ev[stop - 1])       # callers may sync either stream

@@ -8,6 +8,7 @@ scope.
 """
 from __future__ import annotations
 
+import collections
 import glob
 import os
 
@@ -19,7 +20,8 @@ from . import frames as FR
 from . import ply as PLY
 
 _ENGINES: dict = {}
-_CALIBS: dict = {}
+_CALIBS: "collections.OrderedDict" = collections.OrderedDict()
+_CALIBS_MAX = 4
 
 
 def _engine(h, w):
@@ -29,14 +31,39 @@ def _engine(h, w):
     return _ENGINES[key]
 
 
+def calib_fingerprint(calib) -> str:
+    """Content digest of the calibration arrays the path reads (xxh3 over shapes, dtypes and
+    bytes): a cache keyed on it never serves tables of an edited or different calibration."""
+    try:
+        import xxhash
+        h = xxhash.xxh3_64()
+    except ImportError:                     # pragma: no cover - xxhash ships with the image
+        import hashlib
+        h = hashlib.blake2b(digest_size=16)
+    for k in ("cam_K", "Oc", "wPlaneCol", "wPlaneRow", "Nc"):
+        a = calib.get(k) if hasattr(calib, "get") else None
+        if a is None:
+            h.update(f"{k}:none;".encode())
+            continue
+        a = np.ascontiguousarray(a)
+        h.update(f"{k}:{a.shape}:{a.dtype.str};".encode())
+        h.update(memoryview(a).cast("B"))
+    return h.hexdigest()
+
+
 def _device_calib(calib, h, w):
-    """Cache device tables per (calib dict object, geometry)."""
-    key = (id(calib), h, w)
-    hit = _CALIBS.get(key)
-    if hit is not None and hit[0] is calib:
-        return hit[1]
+    """Device tables of ``calib`` for one geometry on the current GPU: a small LRU keyed on
+    (device, geometry, content digest), so it neither pins callers' dicts nor grows without
+    bound, and an edited calibration is uploaded afresh."""
+    key = (torch.cuda.current_device(), h, w, calib_fingerprint(calib))
+    dc = _CALIBS.get(key)
+    if dc is not None:
+        _CALIBS.move_to_end(key)
+        return dc
     dc = E.DeviceCalib(calib, h, w)
-    _CALIBS[key] = (calib, dc)
+    _CALIBS[key] = dc
+    while len(_CALIBS) > _CALIBS_MAX:
+        _CALIBS.popitem(last=False)
     return dc
 
 
@@ -78,7 +105,9 @@ def run_view_folders(subfolders, log, reconstruct, read=None, write=None) -> int
     """The per-folder loop of batch mode (processing.py:314-334) as a three-stage pipeline.
 
     ``read(folder) -> host`` (frame read + PNG decode) runs one folder ahead on a prefetch
-    thread; ``reconstruct(folder, host) -> result`` (H2D, kernels, D2H) on the calling thread;
+    thread; ``reconstruct(folder, get_host) -> result`` (H2D, kernels, D2H) on the calling
+    thread, where ``get_host()`` waits for that folder's read (so the stage can log its
+    progress line first, as the reference does before reading);
     ``write(folder, result) -> out_name`` (ASCII PLY) on a writer thread while the next folder is
     reconstructed.  At most one folder is in each stage.  Per-folder isolation as in the
     reference: an exception in any stage is logged as ``❌ Error in <folder>`` at that folder's
@@ -116,8 +145,8 @@ def run_view_folders(subfolders, log, reconstruct, read=None, write=None) -> int
             k += 1
             prefetch(k)                                  # the next folder with images
             try:
-                host = pending.pop(folder).result() if read is not None else None
-                result = reconstruct(folder, host)
+                fut = pending.pop(folder) if read is not None else None
+                result = reconstruct(folder, fut.result if fut is not None else (lambda: None))
             except Exception as e:  # noqa: BLE001
                 drain()
                 log(f"  ❌ Error in {os.path.basename(folder)}: {e}\n")
@@ -263,13 +292,19 @@ class ProcessingLogic:
 
 def batch_reconstruct_stage(cfg, calib, row_mode, epipolar_tol, log):
     """``reconstruct`` stage of :func:`run_view_folders`: upload + fused kernels -> host cloud,
-    with the reference's progress lines (processing.py:264-272)."""
-    def stage(folder, host):
+    with the reference's progress lines (processing.py:264-272).  The device tables are made
+    once per geometry for the whole batch."""
+    tables = {}
+
+    def stage(folder, get_host):
         log(f"  -> Decoding folder '{os.path.basename(folder)}'  "
             f"[col-sets={cfg.n_sets_col}  row-sets={cfg.n_sets_row}]...")
-        dev, _ = load_capture(folder, cfg, host=host)
+        dev, _ = load_capture(folder, cfg, host=get_host())
         log("  -> Reconstructing 3D points...")
-        points, colors = reconstruct_view(dev, cfg, calib, row_mode, epipolar_tol)
+        geom = (dev.height, dev.width, torch.cuda.current_device())
+        if geom not in tables:
+            tables[geom] = E.DeviceCalib(calib, dev.height, dev.width)
+        points, colors = reconstruct_view(dev, cfg, calib, row_mode, epipolar_tol, dc=tables[geom])
         log(f"  -> Saving {len(points)} points...")
         return points, colors
     return stage
@@ -285,13 +320,14 @@ def batch_write_stage():
 
 
 def reconstruct_view(dev: E.DeviceFrames, cfg: E.DecodeConfig, calib: dict, row_mode=1,
-                     epipolar_tol=2.0, xyz_f64=True):
+                     epipolar_tol=2.0, xyz_f64=True, dc: E.DeviceCalib | None = None):
     """Fused decode + triangulate of one in-HBM capture -> host ``(P, C)`` like the reference
-    pair ``_gray_decode`` + ``_reconstruct_point_cloud``."""
+    pair ``_gray_decode`` + ``_reconstruct_point_cloud``.  ``dc``: device tables of ``calib``
+    already made for this geometry (else looked up in the module cache)."""
     if row_mode not in (0, 1, 2):
         return None
     eng = _engine(dev.height, dev.width)
-    dc = _device_calib(calib, dev.height, dev.width)
+    dc = dc if dc is not None else _device_calib(calib, dev.height, dev.width)
     out = eng.reconstruct(dev, cfg, dc, row_mode, epipolar_tol, xyz_f64=xyz_f64)
     P, C = out.result()
     return P.cpu().numpy(), C.cpu().numpy()

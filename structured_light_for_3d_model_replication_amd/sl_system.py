@@ -69,10 +69,18 @@ class SLSystem:
         cfg = E.DecodeConfig(1920, 1080, variant="slsystem")
         imgs, tex = PR.FR.load_frames(files, texture=True)
         dev = E.DeviceFrames(imgs, tex)
+        # the reference's two steps (sl_system.py:666-669): maps (slg_decode), then the cloud
+        # from the maps (slg_triangulate); the legacy path is not throughput-critical, and the
+        # maps give the valid-pixel count the reference prints (sl_system.py:610)
+        eng = PR._engine(dev.height, dev.width)
         print("Decoding Columns...")
         print("Decoding Rows...")
+        col, row, mask = eng.decode(dev, cfg)
         print("Reconstructing 3D points...")
-        points, colors = PR.reconstruct_view(dev, cfg, calib_data, row_mode=0)
+        print(f"Processing {int(mask.sum().item())} valid pixels...")
+        dc = PR._device_calib(calib_data, dev.height, dev.width)
+        P, C = eng.triangulate(col, row, mask, dev.texture, dc, row_mode=0, xyz_f64=True).result()
+        points, colors = P.cpu().numpy(), C.cpu().numpy()
 
         ply_name = os.path.basename(scan_dir) + ".ply"
         out_path = os.path.join(scan_dir, ply_name)

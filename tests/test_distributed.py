@@ -57,6 +57,20 @@ def _body(rank, tmp, q):
                 assert torch.equal(gb, (torch.arange(m * 3).reshape(m, 3) % 251 + r).to(torch.uint8))
         else:
             assert got is None
+        # exact sizes, strongly ragged: 100003 points from rank 0, one from rank 1 (each
+        # receive buffer is exactly the sender's size: no padding to the largest rank)
+        n = 100003 if rank == 0 else 1
+        xyz = torch.arange(n * 3, dtype=torch.float32).reshape(n, 3) - 7 * rank
+        bgr = (torch.arange(n * 3, dtype=torch.int64).reshape(n, 3) % 241).to(torch.uint8)
+        got = D.gather_clouds(xyz, bgr, dst=1)
+        if rank == 1:
+            assert [g[0].shape[0] for g in got] == [100003, 1]
+            for r, (gx, gb) in enumerate(got):
+                m = 100003 if r == 0 else 1
+                assert torch.equal(gx, torch.arange(m * 3, dtype=torch.float32).reshape(m, 3) - 7 * r)
+                assert torch.equal(gb, (torch.arange(m * 3).reshape(m, 3) % 241).to(torch.uint8))
+        else:
+            assert got is None
         # float64 clouds and an empty rank
         xyz64 = torch.randn(0 if rank else 4, 3, dtype=torch.float64, generator=torch.Generator().manual_seed(1))
         got = D.gather_clouds(xyz64, torch.zeros(xyz64.shape[0], 3, dtype=torch.uint8), dst=0)

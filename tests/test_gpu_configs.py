@@ -1,0 +1,172 @@
+"""GPU parity at the BASELINE configurations' full sizes and at the benchmark's exact launch shape
+(VERDICT r1 "next" #1).  Every check goes through the C ABI and compares with the oracle
+(tests only):
+
+* C2 bench shape: ``BatchReconstructor.run_pipelined(mode="fused")`` over 36 full-size 1920x1080
+  views, 12 per main3 launch, 2 workspace slots, batch k carrying batch k+2's Otsu histograms
+  (per-tile partials -> parts_kernel), issued in two pieces (the stream continuation bench.py
+  uses).  Every view's count equals the oracle's; f32 clouds within the north-star tolerance
+  and f64 clouds bit-exact on a subset; the 1013-tile look-back chains are full length.
+* C3: the 36-view turntable job at 1080p with 11 + 11 bits through the sharded path's pieces
+  (12-view batches, the C-ABI RCCL gatherv at world size 1): every view's count and a subset of
+  clouds (f64, bit for bit) against the oracle, gathered layout checked.
+* C5 geometry: a 3840x2160 view, projector 1920x1080, 11 + 11 bits, row_mode 1 -- maps, f64
+  cloud bit-exact, f32 within tolerance, codes equal the renderer's ground truth; and a 2-view
+  batch of them.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from oracle import sl_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+XYZ32_RTOL = 1e-4     # BASELINE.json north_star: XYZ within 1e-4 relative (fp32 vs float64)
+N_VIEWS = 36
+
+
+def _xyz32_close(got, want):
+    got = np.asarray(got, np.float64)
+    scale = np.maximum(np.abs(want), 1e-3)
+    assert np.all(np.abs(got - want) <= XYZ32_RTOL * scale)
+
+
+@pytest.fixture(scope="module")
+def mods():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a ROCm device")
+    from structured_light_for_3d_model_replication_amd import engine as E, _native as N
+    N.lib()
+    return E, N
+
+
+@pytest.fixture(scope="module")
+def scan():
+    """36 rendered 1080p turntable views (10 degree steps, 46 frames each) + their calibration."""
+    from structured_light_for_3d_model_replication_amd import synth
+    rig = synth.default_rig(1920, 1080, 1920, 1080)
+    with ThreadPoolExecutor(8) as ex:
+        views = list(ex.map(lambda i: synth.render_view(rig, 10.0 * i, seed=500 + i), range(N_VIEWS)))
+    return rig.tables(), views
+
+
+def _oracle_all(cal, views, nsets, row_mode=1):
+    def one(v):
+        c, r, m = O.decode_processing(list(v.frames), n_sets_col=nsets[0], n_sets_row=nsets[1])
+        return O.reconstruct_processing(c, r, m, v.texture, cal, row_mode=row_mode)
+    with ThreadPoolExecutor(8) as ex:
+        return list(ex.map(one, views))
+
+
+def test_c2_bench_launch_shape(mods, scan):
+    """The benchmark's exact shape: 12 C2 views per fused launch, two slots, carried histograms."""
+    E, N = mods
+    import torch
+    cal, views = scan
+    want = _oracle_all(cal, views, (11, 10))
+    dev = [E.DeviceFrames(list(v.frames), v.texture) for v in views]
+    dcal = E.DeviceCalib(cal, 1080, 1920)
+    cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
+    for f64 in (False, True):
+        eng = E.BatchReconstructor(1080, 1920, 12, slots=2)
+        clouds = [E.Cloud(1920 * 1080, 1, f64) for _ in range(N_VIEWS)]
+        batches = [eng.prepare(dev[12 * b:12 * b + 12], cfg, dcal, clouds[12 * b:12 * b + 12], 1, 2.0, slot=b % 2)
+                   for b in range(3)]
+        s_main, s_stats = torch.cuda.Stream(), torch.cuda.Stream()
+        eng.run_pipelined(batches, s_main, s_stats, mode="fused", start=0, stop=1)   # bench: warmup ...
+        eng.run_pipelined(batches, s_main, s_stats, mode="fused", start=1, stop=3)   # ... then timed steps
+        torch.cuda.synchronize()
+        for k, (c, (Po, Co)) in enumerate(zip(clouds, want)):
+            P, C = c.result()
+            assert P.shape[0] == Po.shape[0], (f64, k, P.shape[0], Po.shape[0])
+            if k in (0, 17, 35) or (not f64 and k % 6 == 0):
+                P, C = P.cpu().numpy(), C.cpu().numpy()
+                assert np.array_equal(C, Co), (f64, k)
+                if f64:
+                    assert np.array_equal(P, Po), k
+                else:
+                    _xyz32_close(P, Po)
+        assert all(eng.header(s, v)[3084:3088].cpu().numpy()[0] & 1 == 0 for s in range(2) for v in range(12))
+    assert min(len(w[0]) for w in want) > 500_000
+
+
+def test_c3_sharded_job(mods, scan):
+    """C3: 36 views, 11 + 11 bits, 12-view batches, then the C-ABI RCCL gatherv (world 1)."""
+    E, N = mods
+    import torch
+    from structured_light_for_3d_model_replication_amd import distributed as D
+    cal, views = scan
+    want = _oracle_all(cal, views, (11, 11))
+    dev = [E.DeviceFrames(list(v.frames), v.texture) for v in views]
+    dcal = E.DeviceCalib(cal, 1080, 1920)
+    cfg = E.DecodeConfig(1920, 1080, 11, 11, "otsu")
+    lo, hi = D.shard_range(N_VIEWS, 0, 1)
+    assert (lo, hi) == (0, N_VIEWS)
+    eng = E.BatchReconstructor(1080, 1920, 12, slots=3)
+    clouds = [E.Cloud(1920 * 1080, 1, True) for _ in range(N_VIEWS)]
+    s = torch.cuda.Stream()
+    for b in range(3):
+        eng.run(eng.prepare(dev[12 * b:12 * b + 12], cfg, dcal, clouds[12 * b:12 * b + 12], 1, 2.0, slot=b), stream=s)
+    s.synchronize()
+    parts = []
+    for c, (Po, _) in zip(clouds, want):
+        P, C = c.result()
+        assert P.shape[0] == Po.shape[0]
+        parts.append((P, C))
+    g = D.RcclCloudGather()
+    try:
+        got = g.gather(parts, N_VIEWS, root=0, stream=s)
+        s.synchronize()
+    finally:
+        g.close()
+    assert len(got) == N_VIEWS
+    rx, rb = g.last_buffers
+    assert rx.shape[0] == sum(len(w[0]) for w in want)
+    for k in (0, 9, 18, 27, 35):
+        assert np.array_equal(got[k][0].cpu().numpy(), want[k][0]), k
+        assert np.array_equal(got[k][1].cpu().numpy(), want[k][1]), k
+
+
+def test_c5_full_size(mods):
+    """C5 geometry: 3840x2160 camera, projector 1920x1080, 11 + 11 bits (46 frames), row_mode 1."""
+    E, N = mods
+    import torch
+    from structured_light_for_3d_model_replication_amd import synth
+    rig = synth.default_rig(3840, 2160, 1920, 1080)
+    cal = rig.tables()
+    vs = [synth.render_view(rig, a, seed=31 + i) for i, a in enumerate((15.0, 195.0))]
+    assert vs[0].frames.shape == (46, 2160, 3840)
+    cfg = E.DecodeConfig(1920, 1080, 11, 11, "otsu")
+    dcal = E.DeviceCalib(cal, 2160, 3840)
+    dev = [E.DeviceFrames(list(v.frames), v.texture) for v in vs]
+    eng = E.Reconstructor(2160, 3840)
+    v = vs[0]
+    col, row, mask = eng.decode(dev[0], cfg)
+    oc, orow, om = O.decode_processing(list(v.frames), n_sets_col=11, n_sets_row=11)
+    shape = (2160, 3840)
+    col, row, mask = (col.reshape(shape).cpu().numpy(), row.reshape(shape).cpu().numpy(),
+                      mask.reshape(shape).cpu().numpy().astype(bool))
+    assert np.array_equal(col, oc) and np.array_equal(row, orow) and np.array_equal(mask, om)
+    lit = v.lit & mask
+    assert lit.sum() > 1_000_000
+    assert np.array_equal(col[lit], v.proj_col[lit]) and np.array_equal(row[lit], v.proj_row[lit])
+    Po, Co = O.reconstruct_processing(oc, orow, om, v.texture, cal, row_mode=1)
+    P, C = eng.reconstruct(dev[0], cfg, dcal, 1, xyz_f64=True).result()
+    assert np.array_equal(P.cpu().numpy(), Po) and np.array_equal(C.cpu().numpy(), Co)
+    P, C = eng.reconstruct(dev[0], cfg, dcal, 1, xyz_f64=False).result()
+    assert len(P) == len(Po) and np.array_equal(C.cpu().numpy(), Co)
+    _xyz32_close(P.cpu().numpy(), Po)
+    assert eng.error_flags() & 1 == 0
+    # the 2-view batch of the bench's c5 shape (stats + one fused launch, f32)
+    beng = E.BatchReconstructor(2160, 3840, 2)
+    outs = [E.Cloud(2160 * 3840, 1, False) for _ in vs]
+    beng.run(beng.prepare(dev, cfg, dcal, outs, 1, 2.0))
+    torch.cuda.synchronize()
+    Po2, Co2 = _oracle_all(cal, vs[1:], (11, 11))[0]
+    for o, (Pw, Cw) in zip(outs, [(Po, Co), (Po2, Co2)]):
+        P, C = o.result()
+        assert len(P) == len(Pw) and np.array_equal(C.cpu().numpy(), Cw)
+        _xyz32_close(P.cpu().numpy(), Pw)

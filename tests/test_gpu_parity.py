@@ -116,7 +116,7 @@ def test_lookback_helper_path_bit_exact(name, mods, monkeypatch):
     dev = E.DeviceFrames(list(z["frames"]), z["texture"])
     eng = E.Reconstructor(dev.height, dev.width)
     dc = E.DeviceCalib(cal, dev.height, dev.width)
-    monkeypatch.setenv("SLG_DBG", "32")
+    monkeypatch.setenv("SLG_HELP_AFTER", "0")
     for rm in (0, 1, 2):
         P, C = eng.reconstruct(dev, _cfg(E, z["params"]), dc, row_mode=rm, xyz_f64=True).result()
         assert np.array_equal(P.cpu().numpy(), z[f"P{rm}"]) and np.array_equal(C.cpu().numpy(), z[f"C{rm}"])
@@ -194,6 +194,10 @@ def test_process_multi_ply_batch(tmp_path, mods):
         P, C = O.reconstruct_processing(c, r, m, tex, cal, row_mode=1)
         assert (d / f"{d.name}.ply").read_bytes() == O.ply_bytes(P, C)
     assert any("Error in bad_scan" in s and "Not enough images" in s for s in logs)
+    # the reference logs a folder's progress line before its error (processing.py:322-330)
+    i_dec = next(i for i, s in enumerate(logs) if "Decoding folder 'bad_scan'" in s)
+    i_err = next(i for i, s in enumerate(logs) if "Error in bad_scan" in s)
+    assert i_dec < i_err
     assert any("Skipping empty" in s for s in logs)
     assert logs[-1].startswith("=== Batch Complete: 2/4 succeeded")
 

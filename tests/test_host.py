@@ -185,9 +185,12 @@ def test_run_view_folders_pipeline(tmp_path):
             raise ValueError("Not enough images (got 3, need at least 4).")
         return os.path.basename(f).upper()
 
-    def rec(f, host):
-        assert threading.get_ident() == main and host == os.path.basename(f).upper()
+    def rec(f, get_host):
+        assert threading.get_ident() == main
         seen["rec"].append(os.path.basename(f))
+        logs.append(f"-> Decoding {os.path.basename(f)}")     # the stage logs before the read resolves
+        host = get_host()
+        assert host == os.path.basename(f).upper()
         if f.endswith("gpufail"):
             raise RuntimeError("kernel failed")
         return host
@@ -203,14 +206,21 @@ def test_run_view_folders_pipeline(tmp_path):
     ok = PR.run_view_folders(folders, logs.append, rec, read=read, write=write)
     assert ok == 3
     assert seen["read"] == [n for n in names if n != "empty"]
-    assert seen["rec"] == ["a", "c", "d_gpufail", "e_writefail", "f"]
+    assert seen["rec"] == ["a", "b_readfail", "c", "d_gpufail", "e_writefail", "f"]
     assert seen["write"] == ["A", "C", "E_WRITEFAIL", "F"]
+    # reference order (processing.py:322-330): a folder's progress line, then its error
     assert [s.strip() for s in logs] == [
+        "-> Decoding a",
+        "-> Decoding b_readfail",
         "✔ Saved: a.ply",
         "❌ Error in b_readfail: Not enough images (got 3, need at least 4).",
+        "-> Decoding c",
         "Skipping empty (No images found).",
+        "-> Decoding d_gpufail",
         "✔ Saved: c.ply",
         "❌ Error in d_gpufail: kernel failed",
+        "-> Decoding e_writefail",
+        "-> Decoding f",
         "❌ Error in e_writefail: disk full",
         "✔ Saved: f.ply",
     ]

@@ -216,10 +216,8 @@ def main():
         alg_bytes=9 * n_px + 18 * pts[1])
     os.environ["SLG_DBG"] = "16"
     run("stats_no_otsu", lambda v: eng.stats(dfr[v], cfg))
-    for dbg in (8, 15, 1, 2, 4, 3, 7):
+    for dbg in (1, 2, 4, 3, 7):        # profiling instance (row_mode 1, f32, frames, pinhole)
         os.environ["SLG_DBG"] = str(dbg)
-        run(f"tri_rm1_dbg{dbg}", lambda v: eng.triangulate(maps[v][0], maps[v][1], maps[v][2], dfr[v].texture,
-                                                          dcal, 1, xyz_f64=False, out=clouds[1]))
         run(f"main_rm1_dbg{dbg}", lambda v: eng.decode_triangulate(dfr[v], cfg, dcal, clouds[1], 1),
             pre=lambda v: eng.stats(dfr[v], cfg))
     os.environ.pop("SLG_DBG", None)
