@@ -202,6 +202,20 @@ int32_t slg_decode_stats_partials_batch(int32_t n_views, int32_t height, int32_t
                                         const slg_decode_params *dp, void *workspace,
                                         int64_t ws_stride, void *stream);
 
+/* The streaming turntable pipeline on ONE stream (what BatchReconstructor.run_pipelined
+ * "fused" issues): slg_decode_triangulate_batch_next, plus `n_fin` views whose partials an
+ * EARLIER launch on this stream carried (slices at fin_workspace + v * ws_stride) turned into
+ * thresholds by finishing workgroups at the front of this launch's grid -- the work of
+ * slg_decode_stats_partials_batch without its kernel or a second stream.  Batch k's launch
+ * carries batch k+2 and finishes batch k+1; fin_workspace must not be this launch's own
+ * workspace.  Results are identical to slg_decode_stats_batch. */
+int32_t slg_decode_triangulate_batch_carry(const slg_capture *caps, int32_t n_views,
+                                           const slg_decode_params *dp, const slg_calib *calib,
+                                           const slg_tri_params *tp, void *workspace, int64_t ws_stride,
+                                           const slg_cloud *outs, const slg_capture *next,
+                                           int32_t n_next, void *fin_workspace, int32_t n_fin,
+                                           void *const *timing_events, void *stream);
+
 /* Count (into *mismatches, device int64) the Nc entries that differ bitwise from the cam_K
  * pinhole rays; 0 means SLG_RAYS_PINHOLE reproduces the table exactly. */
 int32_t slg_rays_match_pinhole(const double *rays, int32_t height, int32_t width, double fx,

@@ -91,6 +91,10 @@ EXPORTS = {
                                                   ctypes.POINTER(Calib), ctypes.POINTER(TriParams), c_vp,
                                                   c_i64, ctypes.POINTER(Cloud), ctypes.POINTER(Capture), c_i32,
                                                   ctypes.POINTER(c_vp), c_vp]),
+    "slg_decode_triangulate_batch_carry": (c_i32, [ctypes.POINTER(Capture), c_i32, ctypes.POINTER(DecodeParams),
+                                                   ctypes.POINTER(Calib), ctypes.POINTER(TriParams), c_vp,
+                                                   c_i64, ctypes.POINTER(Cloud), ctypes.POINTER(Capture), c_i32,
+                                                   c_vp, c_i32, ctypes.POINTER(c_vp), c_vp]),
     "slg_decode_stats_partials_batch": (c_i32, [c_i32, c_i32, c_i32, ctypes.POINTER(DecodeParams), c_vp, c_i64,
                                                 c_vp]),
     "slg_ply_write": (c_i64, [ctypes.c_char_p, c_vp, c_vp, c_i64, c_i32]),

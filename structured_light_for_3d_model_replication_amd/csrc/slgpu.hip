@@ -531,24 +531,25 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
 constexpr int kPartsInFlight = 16;
 constexpr int kPartsBlocksMax = 64;         // workgroups per view (each sums a contiguous tile range)
 
-__global__ __launch_bounds__(kBlock) void parts_kernel(StatsParams p) {
-  __shared__ uint32_t hg[512];
-  __shared__ uint32_t s_last;
+// One workgroup's share of "thresholds from partials" for one view: workgroup `block` of
+// `n_blocks` sums its contiguous range of the view's n_parts per-tile partials, adds them into
+// the view's histogram copies, takes a ticket; the last arriver runs Otsu, writes the mask
+// thresholds and resets the histogram state.  Also zeroes the view's look-back words (arming
+// the main launch that will use these thresholds; ordered by the kernel boundary).  256 lanes;
+// hg: 512 words of LDS, s_last: one.  Used by parts_kernel and by main3's finishing workgroups.
+__device__ void otsu_from_parts(const uint32_t* pp, WsHeader* ws, int64_t n_parts, int64_t n_px,
+                                int64_t n_state_words, int64_t pad_zero, int block, int n_blocks,
+                                uint32_t* hg, uint32_t* s_last) {
   const int tid = threadIdx.x, wave = tid >> 6;
-  const int view = blockIdx.y;
-  WsHeader* ws = p.wsv[view];
   uint32_t* hist_part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + kHistPartOff);
-  uint64_t* states = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + states_off(p.n_px));
-  const uint32_t* pp = p.parts[view];
-
-  // Arm the compaction state of the following main launch (ordered by the kernel boundary).
-  for (int64_t i = int64_t(blockIdx.x) * kBlock + tid; i < p.n_state_words; i += int64_t(gridDim.x) * kBlock)
+  uint64_t* states = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + states_off(n_px));
+  for (int64_t i = int64_t(block) * kBlock + tid; i < n_state_words; i += int64_t(n_blocks) * kBlock)
     states[i] = 0;
-  if (blockIdx.x == 0 && tid == 0) ws->tile_counter = 0;
+  if (block == 0 && tid == 0) ws->tile_counter = 0;
 
   // thread t owns packed word t (bins 2t, 2t+1 of [white 0..255 | clip 256..511])
-  const int64_t per = (p.n_parts + gridDim.x - 1) / gridDim.x;
-  const int64_t t0 = int64_t(blockIdx.x) * per, t1 = t0 + per < p.n_parts ? t0 + per : p.n_parts;
+  const int64_t per = (n_parts + n_blocks - 1) / n_blocks;
+  const int64_t t0 = int64_t(block) * per, t1 = t0 + per < n_parts ? t0 + per : n_parts;
   uint32_t a0 = 0, a1 = 0;
   for (int64_t k0 = t0; k0 < t1; k0 += kPartsInFlight) {
     uint32_t v[kPartsInFlight];
@@ -558,7 +559,7 @@ __global__ __launch_bounds__(kBlock) void parts_kernel(StatsParams p) {
 #pragma unroll
     for (int j = 0; j < kPartsInFlight; ++j) { a0 += v[j] & 0xffffu; a1 += v[j] >> 16; }
   }
-  uint32_t* dst = hist_part + (blockIdx.x % kHistCopies) * 512 + 2 * tid;
+  uint32_t* dst = hist_part + (block % kHistCopies) * 512 + 2 * tid;
   if (a0) atomicAdd(dst, a0);
   if (a1) atomicAdd(dst + 1, a1);
 
@@ -568,10 +569,10 @@ __global__ __launch_bounds__(kBlock) void parts_kernel(StatsParams p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t t = __hip_atomic_fetch_add(&ws->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (t == gridDim.x - 1) ? 1u : 0u;
+    *s_last = (t == uint32_t(n_blocks) - 1) ? 1u : 0u;
   }
   __syncthreads();
-  if (!s_last) return;
+  if (!*s_last) return;
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -582,12 +583,12 @@ __global__ __launch_bounds__(kBlock) void parts_kernel(StatsParams p) {
 #pragma unroll
     for (int c = 0; c < kHistCopies; ++c)
       acc += __hip_atomic_load(hist_part + c * 512 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((i & 255) == 0) acc -= uint32_t(p.pad_zero);   // zero padding past n_px
+    if ((i & 255) == 0) acc -= uint32_t(pad_zero);   // zero padding past n_px
     hg[i] = acc;
   }
   __syncthreads();
   if (wave < 2) {                              // wave 0: white, wave 1: clip(w-b); concurrently
-    const double thr = otsu_wave(hg + 256 * wave, p.n_px);
+    const double thr = otsu_wave(hg + 256 * wave, n_px);
     if ((tid & 63) == 0) {
       const int m = int_threshold(thr, wave == 0 ? 0 : -255);
       if (wave == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
@@ -595,6 +596,13 @@ __global__ __launch_bounds__(kBlock) void parts_kernel(StatsParams p) {
   }
   for (int i = tid; i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
   if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
+}
+
+__global__ __launch_bounds__(kBlock) void parts_kernel(StatsParams p) {
+  __shared__ uint32_t hg[512];
+  __shared__ uint32_t s_last;
+  otsu_from_parts(p.parts[blockIdx.y], p.wsv[blockIdx.y], p.n_parts, p.n_px, p.n_state_words, p.pad_zero,
+                  int(blockIdx.x), int(gridDim.x), hg, &s_last);
 }
 
 // ------------------------------------------------------------------ main kernel
@@ -1036,11 +1044,24 @@ struct ViewIO {
   uint32_t* hn_part;          // -> [n_tiles][kPartWords] of this view's workspace slice
 };
 
+// A view whose Otsu partials (carried by an EARLIER launch on the same stream) this launch
+// turns into thresholds, with finishing workgroups placed at the front of its grid: the
+// streaming pipeline's stats pass then costs no kernel and no cross-stream wait of its own.
+struct FinIO {
+  const uint32_t* parts;      // [n_tiles][kPartWords] partials in the view's workspace slice
+  WsHeader* ws;               // the slice: thresholds out, look-back words armed
+};
+
 struct Main3Params {
   MainParams c;               // geometry, decode plan, calibration (per-view pointers unused)
   int32_t n_views;
+  int32_t n_fin;              // views finished by this launch (FinIO), 0: none
+  int32_t fin_blocks;         // finishing workgroups per such view (the grid's first n_fin*fin_blocks)
   int32_t pad;
+  int64_t n_state_words;      // look-back words per view slice (finishing arms them)
+  int64_t pad_zero;           // zero bytes the last tile's partial counted past n_px
   ViewIO v[kMaxViews];
+  FinIO fin[kMaxViews];
 };
 
 static_assert(sizeof(Main3Params) <= 4096, "kernel arguments");
@@ -1171,10 +1192,18 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = int(P.c.n_tiles);
+  const int n_fin_wg = P.n_fin * P.fin_blocks;      // finishing workgroups come first
+  if (int(blockIdx.x) < n_fin_wg) {
+    const int fv = int(blockIdx.x) / P.fin_blocks;
+    otsu_from_parts(P.fin[fv].parts, P.fin[fv].ws, tiles, P.c.n_px, P.n_state_words, P.pad_zero,
+                    int(blockIdx.x) - fv * P.fin_blocks, P.fin_blocks, s_code, s_bgr);
+    return;
+  }
+  const int bid = int(blockIdx.x) - n_fin_wg;
   // Views interleaved in dispatch order: each view's look-back chain has only ~1/n_views of
   // the resident workgroups in flight, so a tile waits on fewer, similar predecessors.
-  const int tile = int(blockIdx.x) / P.n_views;
-  const int view = int(blockIdx.x) - tile * P.n_views;
+  const int tile = bid / P.n_views;
+  const int view = bid - tile * P.n_views;
   const MainParams p = view_params(P, view);
   const int64_t tile_px = int64_t(tile) * kTilePx;
   const int64_t px0 = tile_px + int64_t(tid) * kPx;
@@ -1377,7 +1406,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     stamp(3);
     if (tid == 0) {
       rec[6] = uint32_t(n_items);
-      uint4* out = reinterpret_cast<uint4*>(reinterpret_cast<char*>(P.v[0].ws) + parts_off(p.n_px)) + 2 * blockIdx.x;
+      uint4* out = reinterpret_cast<uint4*>(reinterpret_cast<char*>(P.v[0].ws) + parts_off(p.n_px)) + 2 * bid;
       out[0] = make_uint4(rec[0], rec[1], rec[2], rec[3]);
       out[1] = make_uint4(rec[4], rec[5], rec[6], rec[7]);
     }
@@ -1651,7 +1680,7 @@ int launch_main3(Main3Fn fn, Main3Params& mp, const slg_tri_params* tp, const sl
                                             "row_mode 1, f32, frames, pinhole only)");
   mp.c.dbg = debug_flags();
   mp.c.help_after = help_after();
-  const int64_t grid = mp.c.n_tiles * mp.n_views;
+  const int64_t grid = int64_t(mp.n_fin) * mp.fin_blocks + mp.c.n_tiles * mp.n_views;
   if (grid > INT_MAX) return fail(SLG_ERR_UNSUPPORTED, "batch too large for one launch");
   hipLaunchKernelGGL(fn, dim3(unsigned(grid)), dim3(kTileBlock), 0, s, mp);
   int rc = check_launch("main kernel");
@@ -1686,10 +1715,15 @@ int check_batch(const slg_capture* caps, int n_views) {
 // slice): one main3 launch per kMaxViews views.  timing_events: 2 per launch, or NULL.
 int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* dp, const slg_calib* calib,
                 const slg_tri_params* tp, char* ws, int64_t ws_stride, const slg_cloud* outs,
-                void* const* timing_events, hipStream_t s, const slg_capture* next = nullptr, int n_next = 0) {
+                void* const* timing_events, hipStream_t s, const slg_capture* next = nullptr, int n_next = 0,
+                char* fin_ws = nullptr, int n_fin = 0) {
   if (!caps || n_views < 1 || !dp || !ws || !outs) return fail(SLG_ERR_INVALID, "NULL argument");
   int rc = check_batch(caps, n_views);
   if (rc) return rc;
+  if (n_fin) {                                      // finish thresholds carried by an earlier launch
+    if (!fin_ws || n_fin < 0 || n_fin > kMaxViews) return fail(SLG_ERR_INVALID, "finish: NULL or more than 16 views");
+    if (dp->thresh_mode != SLG_THRESH_OTSU) return fail(SLG_ERR_UNSUPPORTED, "carried histograms need thresh_mode OTSU");
+  }
   if (n_next) {                                     // the batch after next rides along (Otsu only)
     if (!next || n_next < 0 || n_next > n_views) return fail(SLG_ERR_INVALID, "next batch: NULL or more views than this batch");
     if (dp->thresh_mode != SLG_THRESH_OTSU) return fail(SLG_ERR_UNSUPPORTED, "next-batch histograms need thresh_mode OTSU");
@@ -1735,6 +1769,18 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
         io.hn_white = next[v].frames;
         io.hn_black = next[v].frames + next[v].frame_stride;
         io.hn_part = reinterpret_cast<uint32_t*>(ws + int64_t(v) * ws_stride + parts_off(n_px));
+      }
+    }
+    mp.n_fin = launch == 0 ? n_fin : 0;             // the first launch finishes them all
+    if (mp.n_fin) {
+      const int64_t nb = (mp.c.n_tiles + 127) / 128;   // ~128 partials (128 KB) per workgroup
+      mp.fin_blocks = int(nb < 1 ? 1 : (nb > kPartsBlocksMax ? kPartsBlocksMax : nb));
+      mp.n_state_words = n_state_words(n_px);
+      mp.pad_zero = mp.c.n_tiles * kTilePx - n_px;
+      for (int k = 0; k < n_fin; ++k) {
+        char* slice = fin_ws + int64_t(k) * ws_stride;
+        mp.fin[k].parts = reinterpret_cast<const uint32_t*>(slice + parts_off(n_px));
+        mp.fin[k].ws = reinterpret_cast<WsHeader*>(slice);
       }
     }
     if (timing_events && timing_events[2 * launch]) (void)hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * launch]), s);
@@ -2054,6 +2100,17 @@ int32_t slg_decode_triangulate_batch_next(const slg_capture* caps, int32_t n_vie
                                           int32_t n_next, void* const* timing_events, void* stream) {
   return fused_batch(caps, n_views, dp, calib, tp, static_cast<char*>(workspace), ws_stride, outs, timing_events,
                      static_cast<hipStream_t>(stream), next, next ? n_next : 0);
+}
+
+int32_t slg_decode_triangulate_batch_carry(const slg_capture* caps, int32_t n_views, const slg_decode_params* dp,
+                                           const slg_calib* calib, const slg_tri_params* tp, void* workspace,
+                                           int64_t ws_stride, const slg_cloud* outs, const slg_capture* next,
+                                           int32_t n_next, void* fin_workspace, int32_t n_fin,
+                                           void* const* timing_events, void* stream) {
+  if (n_fin > 1 && (ws_stride & 255)) return fail(SLG_ERR_INVALID, "ws_stride not 256-aligned");
+  return fused_batch(caps, n_views, dp, calib, tp, static_cast<char*>(workspace), ws_stride, outs, timing_events,
+                     static_cast<hipStream_t>(stream), next, next ? n_next : 0, static_cast<char*>(fin_workspace),
+                     fin_workspace ? n_fin : 0);
 }
 
 int32_t slg_decode_stats_partials_batch(int32_t n_views, int32_t height, int32_t width, const slg_decode_params* dp,

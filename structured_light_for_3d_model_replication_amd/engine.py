@@ -402,30 +402,52 @@ class BatchReconstructor:
             self.ws_stride, pb.clouds, nxt.caps, nxt.n, self._events_arg(pb, events), _stream(stream)))
         pb.launched_on(stream)
 
+    def main_carry(self, pb: PreparedBatch, nxt: PreparedBatch | None, fin: PreparedBatch | None,
+                   events=None, stream=None):
+        """Fused launch of ``pb`` that carries ``nxt``'s histograms (the batch after next, same
+        slot) and finishes ``fin``'s thresholds from the partials an earlier launch on this
+        stream left in ``fin``'s slot (``slg_decode_triangulate_batch_carry``)."""
+        if nxt is not None and (nxt.slot != pb.slot or nxt.n > pb.n):
+            raise ValueError("the carried batch must use this batch's slot and have no more views")
+        if fin is not None and (fin.slot == pb.slot or fin.n > MAX_VIEWS_PER_LAUNCH):
+            raise ValueError("the finished batch must use another slot and have <= 16 views")
+        N.check(N.lib().slg_decode_triangulate_batch_carry(
+            pb.caps, pb.n, ctypes.byref(pb.dp), ctypes.byref(pb.calib), ctypes.byref(pb.tp), self._ws(pb.slot),
+            self.ws_stride, pb.clouds, nxt.caps if nxt is not None else None, nxt.n if nxt is not None else 0,
+            self._ws(fin.slot) if fin is not None else None, fin.n if fin is not None else 0,
+            self._events_arg(pb, events), _stream(stream)))
+        pb.launched_on(stream)
+
     def stats_partials(self, pb: PreparedBatch, stream=None):
         """Thresholds of ``pb`` from the partials a fused launch left in its slot."""
         N.check(N.lib().slg_decode_stats_partials_batch(pb.n, self.height, self.width, ctypes.byref(pb.dp),
                                                         self._ws(pb.slot), self.ws_stride, _stream(stream)))
 
-    def run_pipelined(self, batches, main_stream, stats_stream, events=None, mode="fused",
+    @staticmethod
+    def _carried(batches, j) -> bool:
+        """Whether batch j's histograms ride on batch j-2's fused launch (same slot, no more views)."""
+        return (j >= 2 and batches[j].slot == batches[j - 2].slot and batches[j].n <= batches[j - 2].n
+                and batches[j].n <= MAX_VIEWS_PER_LAUNCH)
+
+    def run_pipelined(self, batches, main_stream, stats_stream=None, events=None, mode="fused",
                       start=0, stop=None):
         """Launch ``batches[start:stop]`` (PreparedBatch list; consecutive ones on different
-        slots) with their stats off the fused launches' critical path.
+        slots) with their Otsu stats off the critical path.
 
+        mode "fused" (ONE stream): batch k's fused launch also counts batch k+2's histograms
+        (per-tile partials, no second pass over its white/black frames) and, with workgroups at
+        the front of its grid, turns the partials batch k-1's launch left for batch k+1 into
+        thresholds -- no stats kernel and no cross-stream wait between launches.  Needs Otsu
+        thresholds and slots alternating k % 2; the first two batches (and any batch with more
+        views than the one that would carry it) get a regular stats pass.
         mode "overlap": the stats pass of batch k+1 runs on ``stats_stream`` beside batch k's
         fused launch on ``main_stream``.
-        mode "fused": batch k's fused launch also computes batch k+2's Otsu histograms (per-tile
-        partials, no second pass over its white/black frames); a small kernel on
-        ``stats_stream`` turns them into thresholds beside batch k+1's launch.  Needs Otsu
-        thresholds and slots alternating k % 2; the first two batches (and any batch with more
-        views than the one carrying it) get a regular stats pass.
 
         The list is a stream: a call with ``start > 0`` continues the pipeline where the call
-        that stopped at ``start`` left it (the thresholds of batches ``start`` and ``start+1``
-        were armed by that call), so a long run can be issued in pieces -- e.g. warmup and timed
-        steps -- without restarting it.  Batches past ``stop`` are only prepared for (their
-        stats / histograms), never launched.  ``events[k - start]``: timing events for batch
-        k's fused launches, or None."""
+        that stopped at ``start`` left it, so a long run can be issued in pieces -- e.g. warmup
+        and timed steps -- without restarting it.  Batches past ``stop`` are only prepared for
+        (their histograms / thresholds), never launched.  ``events[k - start]``: timing events
+        for batch k's fused launches, or None."""
         n = len(batches)
         stop = n if stop is None else min(int(stop), n)
         if not 0 <= start <= stop:
@@ -433,36 +455,27 @@ class BatchReconstructor:
         for k in range(1, n):
             if batches[k].slot == batches[k - 1].slot:
                 raise ValueError("consecutive batches must use different workspace slots")
-        while len(self._events) < 2 * n:
-            self._events.append(torch.cuda.Event())
-        st_ev, mn_ev = self._events[0::2], self._events[1::2]
 
         def ev_of(k):
             return None if events is None else events[k - start]
 
         if mode == "fused" and n and all(b.dp.thresh_mode == N.THRESH_OTSU for b in batches):
+            s = main_stream
             if start == 0:
                 for k in range(min(2, n)):
-                    self.stats(batches[k], stream=stats_stream)
-                    st_ev[k].record(stats_stream)
+                    self.stats(batches[k], stream=s)
             for k in range(start, stop):
-                nxt = batches[k + 2] if k + 2 < n else None
-                carry = nxt is not None and nxt.slot == batches[k].slot and nxt.n <= batches[k].n
-                main_stream.wait_event(st_ev[k])
-                if carry:
-                    self.main_next(batches[k], nxt, events=ev_of(k), stream=main_stream)
-                else:
-                    self.main(batches[k], events=ev_of(k), stream=main_stream)
-                mn_ev[k].record(main_stream)
-                if nxt is not None:                        # batch k+2 reuses batch k's slot
-                    stats_stream.wait_event(mn_ev[k])
-                    (self.stats_partials if carry else self.stats)(nxt, stream=stats_stream)
-                    st_ev[k + 2].record(stats_stream)
-            if stop > start:
-                stats_stream.wait_event(mn_ev[stop - 1])
+                nxt = batches[k + 2] if k + 2 < n and self._carried(batches, k + 2) else None
+                fin = batches[k + 1] if k + 1 < n and self._carried(batches, k + 1) else None
+                self.main_carry(batches[k], nxt, fin, events=ev_of(k), stream=s)
+                if k + 2 < n and nxt is None:              # not carried: a regular pass, after
+                    self.stats(batches[k + 2], stream=s)   # batch k is done with the slot
             return
         if mode not in ("fused", "overlap"):
             raise ValueError(f"unknown pipeline mode {mode!r}")
+        while len(self._events) < 2 * n:
+            self._events.append(torch.cuda.Event())
+        st_ev, mn_ev = self._events[0::2], self._events[1::2]
         if n and start == 0:
             self.stats(batches[0], stream=stats_stream)
             st_ev[0].record(stats_stream)

@@ -488,3 +488,23 @@ def test_partial_histograms_match_frame_stats(mods, hw):
     for v in range(nv):
         assert torch.equal(fields(v), want[v]), (v, ref[v])
     assert any(r > 0 for r in ref)
+    # the same thresholds from the finishing workgroups of a later fused launch on one stream
+    # (slg_decode_triangulate_batch_carry): slot 1 runs its own batch and finishes slot 0's
+    eng2 = E.BatchReconstructor(H, W, nv, slots=2)
+    pb0 = eng2.prepare(frames, cfg, dc, outs, row_mode=1, slot=0)
+    outs1 = [E.Cloud(H * W, 1, False) for _ in range(nv)]
+    pb1 = eng2.prepare(frames, cfg, dc, outs1, row_mode=1, slot=1)
+    eng2.stats(pb0)
+    eng2.stats(pb1)
+    eng2.main_carry(pb0, pb0, None)                  # carries slot 0's own captures
+    for v in range(nv):
+        eng2.header(0, v)[3088:3120] = 0x55
+    eng2.main_carry(pb1, None, pb0)                  # finishes slot 0 at the front of its grid
+    torch.cuda.synchronize()
+    fields2 = lambda v: torch.cat([eng2.header(0, v)[3088:3096], eng2.header(0, v)[3104:3120]])
+    for v in range(nv):
+        assert torch.equal(fields2(v), want[v]), v
+    eng2.main(pb0)                                   # the finished slot is armed: its launch works
+    torch.cuda.synchronize()
+    for o, o1 in zip(outs, outs1):
+        assert torch.equal(o.result()[0], o1.result()[0])
