@@ -537,7 +537,7 @@ constexpr int kPartsBlocksMax = 64;         // workgroups per view (each sums a 
 // thresholds and resets the histogram state.  Also zeroes the view's look-back words (arming
 // the main launch that will use these thresholds; ordered by the kernel boundary).  256 lanes;
 // hg: 512 words of LDS, s_last: one.  Used by parts_kernel and by main3's finishing workgroups.
-__device__ void otsu_from_parts(const uint32_t* pp, WsHeader* ws, int64_t n_parts, int64_t n_px,
+__device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint32_t* pp, WsHeader* ws, int64_t n_parts, int64_t n_px,
                                 int64_t n_state_words, int64_t pad_zero, int block, int n_blocks,
                                 uint32_t* hg, uint32_t* s_last) {
   const int tid = threadIdx.x, wave = tid >> 6;
@@ -648,7 +648,7 @@ struct MainParams {
   uint8_t* scratch_bgr;
   int32_t dbg;             // env SLG_DBG; read only by the profiling instance (PROF): bit0 no
                            // look-back wait, bit1 trivial triangulation, bit2 no output stores,
-                           // bit6 per-workgroup phase records, bits 8-15 look-back back-off cap
+                           // bit3 no BGR stores, bit6 per-workgroup phase records, bit7 no XYZ stores
   uint32_t help_after;     // look-back: s_sleep(2) units before a silent predecessor is helped
                            // (kHelpAfter; env SLG_HELP_AFTER=0 forces the helper path in tests)
 };
@@ -916,7 +916,7 @@ __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int ag
     return true;
   }
   if (lane == 0) st_state(&st[tile], kFlagAgg | uint64_t(agg));   // a helper only ever writes this same value
-  const unsigned nap_cap = PROF && ((p.dbg >> 8) & 0xff) ? (p.dbg >> 8) & 0xff : kNapCap;   // dbg bits 8-15: A/B
+  const unsigned nap_cap = kNapCap;
   const unsigned help_after = p.help_after;
   uint64_t excl = 0;
   int64_t j = tile - 1;
@@ -1181,14 +1181,17 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   constexpr int NS = ROW_MODE == 2 ? 2 : 1;
   constexpr int kB = kTileBlock;
   constexpr int kIt = kTilePx / kB;        // 8 item rounds of one workgroup at most
-  __shared__ uint32_t s_code[kTilePx];     // valid item: col | row << 16
+  __shared__ __attribute__((aligned(16))) uint32_t s_code[kTilePx];   // valid item: col | row << 16
   __shared__ uint32_t s_bgr[kTilePx];      // its BGR (24 bits)
-  __shared__ uint32_t s_uv[kTilePx];       // its pixel coordinates u | v << 16
+  __shared__ __attribute__((aligned(16))) uint32_t s_uv[kTilePx];     // its pixel coordinates u | v << 16
   __shared__ int s_wtot[kB / 64];
   __shared__ int s_cnt[NS][kIt][kB / 64];  // kept points per (round, wave)
   __shared__ uint64_t s_excl[NS];
-  __shared__ __attribute__((aligned(16))) uint2 s_hstage[(kB / 64) * 256];   // next-batch nibble planes
-  __shared__ uint32_t s_hn[512];                                             // next-batch histograms
+  // after phase B the item arrays are dead (only s_bgr is read again): the carried batch's
+  // nibble planes and histograms reuse them, so the workgroup needs 24 KB of LDS, not 35
+  uint2* const s_hstage = reinterpret_cast<uint2*>(s_uv);            // [wave][4 planes][64 lanes]
+  uint32_t* const s_hn = s_code;                                      // [512] histograms
+  static_assert((kB / 64) * 256 * sizeof(uint2) <= sizeof(s_uv) && 512 <= kTilePx, "aliases");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = int(P.c.n_tiles);
@@ -1229,7 +1232,6 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   uint2 hn_w, hn_b;
   if (hn) {
     hist_next_load(P.v[view].hn_white, P.v[view].hn_black, p.n_px, px0, hn_w, hn_b);
-    for (int i = tid; i < 512; i += kB) s_hn[i] = 0;   // ordered before phase C by block_scan's barrier
   }
   // ------------------------------------------------------------ A: decode + tile compaction
   int n_items;
@@ -1338,7 +1340,11 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       }
     }
   }
-  if (hn) hist_next_stage(hn_w, hn_b, p.n_px, px0, s_hstage);
+  if (hn) {                                          // block-uniform
+    __syncthreads();                                 // every wave is past its phase-B item reads
+    for (int i = tid; i < 512; i += kB) s_hn[i] = 0;
+    hist_next_stage(hn_w, hn_b, p.n_px, px0, s_hstage);
+  }
   __syncthreads();
 
   stamp(1);
@@ -1395,8 +1401,12 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       if ((km[s][i] >> lane) & 1ull) {
         const int64_t q = base + before + __popcll(km[s][i] & lt);
         const uint32_t c = s_bgr[tid + kB * i];
-        gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
-        gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
+        if (!(PROF && (p.dbg & 128))) {              // PROF ablation bit 7: no XYZ stores
+          gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
+        }
+        if (!(PROF && (p.dbg & 8))) {                // PROF ablation bit 3: no BGR stores
+          gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
+        }
       }
       base += round;
     }
@@ -1640,7 +1650,7 @@ int debug_flags() {   // profiling ablations only; unset in production
   return e ? atoi(e) : 0;
 }
 
-constexpr int kMainDbgBits = 1 | 2 | 4 | 64 | 0xff00;   // bits main3's profiling instance reads
+constexpr int kMainDbgBits = 1 | 2 | 4 | 8 | 64 | 128;   // bits main3's profiling instance reads
 
 uint32_t help_after() {   // look-back helper delay; SLG_HELP_AFTER=0 forces the helper (tests)
   const char* e = getenv("SLG_HELP_AFTER");

@@ -1,0 +1,125 @@
+#!/usr/bin/env python
+"""A/B of libslgpu.so builds on the benchmark's exact shape (C2, 12 views per fused launch,
+single-stream carried-histogram pipeline), one subprocess per variant, rounds interleaved.
+
+    python tools/ab.py --libs build_ab/base.so,build_ab/w5b6.so [--rounds 3] [--launches 200]
+
+Each worker loads the same cached rendered views (rendered once into /tmp), runs warmup + timed
+launches with HIP events on the launch stream, and checks every view's point count and the
+clouds' bitwise checksum against the first variant's (so a faster-but-wrong build shows up).
+Prints one JSON summary line (median over rounds of each variant's median launch time).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CACHE = "/tmp/slg_ab_views.npz"
+
+
+def worker(a):
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import torch
+    from structured_light_for_3d_model_replication_amd import engine as E, synth
+    W, H = 1920, 1080
+    rig = synth.default_rig(W, H, 1920, 1080)
+    if os.path.exists(CACHE):
+        z = np.load(CACHE)
+        frames, tex = z["frames"], z["tex"]
+    else:
+        vs = [synth.render_view(rig, 30.0 * i, seed=i, n_present=44) for i in range(12)]
+        frames = np.stack([v.frames for v in vs])
+        tex = np.stack([v.texture for v in vs])
+        np.savez(CACHE + ".tmp.npz", frames=frames, tex=tex)
+        os.replace(CACHE + ".tmp.npz", CACHE)
+    cal = rig.tables()
+    dev = torch.device("cuda", 0)
+    pool = [E.DeviceFrames(list(frames[i]), tex[i], device=dev) for _ in range(3) for i in range(12)]
+    dcal = E.DeviceCalib(cal, H, W, device=dev)
+    cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
+    B = 12
+    beng = E.BatchReconstructor(H, W, B, device=dev, slots=2)
+    clouds = [[E.Cloud(H * W, 1, False, device=dev) for _ in range(B)] for _ in range(2)]
+    preps = {}
+
+    def prep(b):
+        key = (b % 3, b % 2)
+        if key not in preps:
+            preps[key] = beng.prepare(pool[12 * (b % 3): 12 * (b % 3) + 12], cfg, dcal, clouds[b % 2], 1, 2.0, slot=b % 2)
+        return preps[key]
+
+    n = a.warmup + a.launches + 2
+    batches = [prep(b) for b in range(n)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.launches)]
+    for x, y in ev:
+        x.record()
+        y.record()
+    s = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize()
+    beng.run_pipelined(batches, s, None, mode="fused", start=0, stop=a.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    beng.run_pipelined(batches, s, None, events=[(x.cuda_event, y.cuda_event) for x, y in ev], mode="fused",
+                       start=a.warmup, stop=a.warmup + a.launches)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / a.launches * 1e6
+    us = sorted(x.elapsed_time(y) * 1e3 for x, y in ev)
+    last = a.warmup + a.launches - 1
+    cl = clouds[last % 2]
+    counts = [int(c.count.item()) for c in cl]
+    chk = float(sum(c.xyz[: int(c.count.item())].double().sum().item() for c in cl))
+    err = int(np.frombuffer(beng.header(0, 0)[3084:3088].cpu().numpy().tobytes(), np.uint32)[0])
+    print(json.dumps({"lib": os.environ.get("SLG_LIB", "default"), "median_us": round(statistics.median(us), 2),
+                      "p10_us": round(us[len(us) // 10], 2), "p90_us": round(us[9 * len(us) // 10], 2),
+                      "wall_us_per_launch": round(wall, 2), "counts": counts, "checksum": chk, "err": err}),
+          flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", default="")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--launches", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--worker", action="store_true")
+    ap.add_argument("--timeout", type=int, default=240)
+    a = ap.parse_args()
+    if a.worker:
+        return worker(a)
+    libs = [x for x in a.libs.split(",") if x] or [""]
+    res = {lib: [] for lib in libs}
+    ref = None
+    for r in range(a.rounds):
+        for lib in libs:
+            env = dict(os.environ)
+            if lib:
+                env["SLG_LIB"] = lib
+            cmd = [sys.executable, __file__, "--worker", "--launches", str(a.launches), "--warmup", str(a.warmup)]
+            p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout)
+            if p.returncode != 0:
+                print(f"[ab] {lib} round {r} FAILED rc={p.returncode}\n{p.stderr[-3000:]}", file=sys.stderr, flush=True)
+                sys.exit(1)
+            line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+            d = json.loads(line)
+            if ref is None:
+                ref = (d["counts"], d["checksum"])
+            d["same_as_first"] = (d["counts"], d["checksum"]) == ref
+            res[lib].append(d)
+            print(f"[ab] round {r} {lib or 'default'}: median {d['median_us']} us  wall {d['wall_us_per_launch']} us  "
+                  f"same={d['same_as_first']} err={d['err']}", file=sys.stderr, flush=True)
+    summ = {lib or "default": {"median_us": statistics.median(x["median_us"] for x in v),
+                               "wall_us": statistics.median(x["wall_us_per_launch"] for x in v),
+                               "all_same": all(x["same_as_first"] for x in v), "errs": [x["err"] for x in v]}
+            for lib, v in res.items()}
+    print(json.dumps(summ), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -96,8 +96,7 @@ def main():
         os.environ.pop("SLG_DBG")
         tags = [("", None)]
         if nb == len(dfr):
-            tags += [(f"_dbg{d}", str(d)) for d in (1, 2, 4, 7)]
-            tags += [(f"_nap{c}", str(c << 8)) for c in (1, 2, 4, 16, 64)]
+            tags += [(f"_dbg{d}", str(d)) for d in (1, 2, 4, 3, 5, 6, 7, 8, 128, 11, 131)]
         for tag, dbg in tags:
             if dbg:
                 os.environ["SLG_DBG"] = dbg
