@@ -155,6 +155,10 @@ def main():
                     help="serial: stats + fused launch per batch on one stream; overlap: the next "
                          "batch's stats on a side stream during this batch's fused launch; fused: "
                          "batch k's fused launch computes batch k+2's histograms")
+    ap.add_argument("--settle-ms", type=float, default=60.0,
+                    help="untimed launches (ms of GPU time) before the warmup, for the clocks to ramp")
+    ap.add_argument("--kernel-events", choices=["launch", "region"], default="region",
+                    help="HIP events per fused launch, or one pair around the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
@@ -233,7 +237,10 @@ def main():
     # the whole run as ONE batch stream: warmup + timed + 2 look-ahead batches whose thresholds
     # the last timed launches prepare (carried histograms), as every other step does
     batches = [prep(b * B, b % 2) for b in range(Wm + K + 2)]
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    # HIP events on the launch stream: one pair per fused launch ("launch": kernel time alone),
+    # or one pair around the timed region ("region": launches + the gaps between them)
+    n_ev = K if args.kernel_events == "launch" else 1
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
     for a, b in ev:                                  # materialise the HIP events
         a.record(s_main)
         b.record(s_main)
@@ -254,6 +261,16 @@ def main():
             for k in range(lo, hi):
                 beng.run(batches[k], events=None if events is None else events[k - lo], stream=s_main)
 
+    # settle: the GPU's clocks ramp under load; the same launches, untimed, for args.settle_ms
+    # of GPU time before the pipeline starts (then the cold start, warmup and timed steps)
+    settle = max(0, int(round(args.settle_ms / 0.35)))
+    if settle:
+        sb = [prep(b * B, b % 2) for b in range(settle + 2)]
+        if args.pipeline in ("overlap", "fused"):
+            beng.run_pipelined(sb, s_main, s_stats, mode=args.pipeline, start=0, stop=settle)
+        else:
+            for k in range(settle):
+                beng.run(sb[k], stream=s_main)
     # cold start: the priming stats passes + the first launch, alone (not part of the metric)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -266,7 +283,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_range(Wm, Wm + K, events=[(a.cuda_event, b.cuda_event) for a, b in ev])
+    if args.kernel_events == "launch":
+        run_range(Wm, Wm + K, events=[(a.cuda_event, b.cuda_event) for a, b in ev])
+    else:
+        ev[0][0].record(s_main)
+        run_range(Wm, Wm + K)
+        ev[0][1].record(s_main)
     t_enq = time.perf_counter() - t0              # host time to enqueue the K steps
     torch.cuda.synchronize()
     if world > 1:
@@ -333,6 +355,8 @@ def main():
                 if traffic_view else None,
                 "kernel": f"main3_kernel<1,{int(f64)},1,1> (fused decode+triangulate+compaction, {B} views per launch)",
                 "kernel_avg_us": round(kern_avg_s * 1e6, 2),
+                "kernel_time": ("HIP events around each fused launch on its stream" if args.kernel_events == "launch"
+                                else "HIP events around the timed region / steps (gaps included)"),
                 "alg_bytes_per_launch": round(bytes_sum / launches)}
         out = {
             "metric": METRIC,
@@ -351,6 +375,8 @@ def main():
                        "step": f"one batch of {B} views: one fused launch + its thresholds (steady-state pipeline)",
                        "us_per_view": round(dt_max / (K * B) * 1e6, 3),
                        "cold_start_ms": round(cold_ms, 3),
+                       "settle_launches": settle,
+                       "kernel_events": args.kernel_events,
                        "views_per_rank": len(views), "device_pool": P, "points_per_view": int(np.mean(pts)),
                        "batch_views": B,
                        "stats_pipeline": args.pipeline,

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define SLG_ABI_VERSION 1
+#define SLG_ABI_VERSION 2
 
 #define SLG_OK 0
 #define SLG_ERR_INVALID 1      /* bad argument (message in slg_last_error) */
@@ -109,6 +109,10 @@ typedef struct slg_calib {
   const double *row_planes;/* device (n_row_planes, 4) row-major = wPlaneRow.T */
   int32_t n_row_planes;
   int32_t reserved3;
+  /* Optional (NULL: the kernels compute numer per point; same values either way): */
+  const double *col_planes_num; /* device (n_col_planes, 4): col_planes with column 3 replaced by
+                                 * numer = ((n0*Oc0 + n1*Oc1) + n2*Oc2) + d (processing.py:163-165) */
+  const double *row_planes_num; /* the same for the row planes (read by row_mode 2 only) */
 } slg_calib;
 
 typedef struct slg_tri_params {

@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 if os.environ.get("SLG_LIB"):            # A/B builds of the same ABI (tools/kbench.py); in-tree only
     LIB_PATH = os.path.abspath(os.environ["SLG_LIB"])
 
+ABI_VERSION = 2          # SLG_ABI_VERSION in include/slgpu.h
 SLG_OK = 0
 SLG_ERR_INVALID = 1
 SLG_ERR_HIP = 2
@@ -47,7 +48,7 @@ class Calib(ctypes.Structure):
                 ("fx", c_dbl), ("fy", c_dbl), ("cx", c_dbl), ("cy", c_dbl),
                 ("oc", c_dbl * 3), ("col_planes", c_vp), ("n_col_planes", c_i32),
                 ("reserved2", c_i32), ("row_planes", c_vp), ("n_row_planes", c_i32),
-                ("reserved3", c_i32)]
+                ("reserved3", c_i32), ("col_planes_num", c_vp), ("row_planes_num", c_vp)]
 
 
 class TriParams(ctypes.Structure):
@@ -132,7 +133,7 @@ def lib():
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
-        if h.slg_version() != 1:
+        if h.slg_version() != ABI_VERSION:
             raise ImportError("libslgpu ABI version mismatch")
         _lib = h
     return _lib

@@ -49,32 +49,36 @@ def stripe_planes(K2: np.ndarray, R: np.ndarray, T: np.ndarray,
     """Projector column/row light planes in camera coordinates, each row ``[nx, ny, nz, d]``.
 
     Geometry of ``server/sl_system.py:379-410``: the plane of projector column ``c`` holds the
-    projector centre ``C = -R^T T`` and the back-projected pixels ``(c, 0)`` and ``(c, PH)``;
+    projector centre ``C = (-R^T) T`` and the back-projected pixels ``(c, 0)`` and ``(c, PH)``;
     a row plane holds ``(0, r)`` and ``(PW, r)``.  ``n = normalize(r1 x r2)``, ``d = -n.C``.
     Returns ``(col_planes (PW,4), row_planes (PH,4))``.
+
+    Bit-identical with the reference: every plane goes through the same NumPy operations on the
+    same shapes as ``get_plane_from_proj_line`` -- a (3,3) @ (3,1) matmul per ray, ``np.cross``
+    of 1-D vectors, ``np.linalg.norm`` and ``np.dot`` of 1-D vectors (BLAS ddot) -- because a
+    batched form rounds differently in the last bit (matmul / norm / dot take other kernels).
+    The ~3000 planes of a rig take ~0.1 s, once per calibration.
     """
-    fxp, fyp, cxp, cyp = float(K2[0, 0]), float(K2[1, 1]), float(K2[0, 2]), float(K2[1, 2])
+    K2 = np.asarray(K2, dtype=np.float64)
+    fxp, fyp, cxp, cyp = K2[0, 0], K2[1, 1], K2[0, 2], K2[1, 2]     # NumPy scalars, as the reference
     Rinv = np.asarray(R, dtype=np.float64).T
-    C = -(Rinv @ np.asarray(T, dtype=np.float64).reshape(3, 1)).ravel()
+    C = (-Rinv @ np.asarray(T, dtype=np.float64).reshape(3, 1)).flatten()   # (-R^T) @ T
 
-    def planes(a_x, a_y, b_x, b_y):
-        p1 = np.stack([a_x, a_y, np.ones_like(a_x)])            # (3, n)
-        p2 = np.stack([b_x, b_y, np.ones_like(b_x)])
-        r1 = Rinv @ p1
-        r2 = Rinv @ p2
-        nrm = np.cross(r1.T, r2.T)                                # (n, 3)
-        nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
-        d = -(nrm @ C)
-        return np.concatenate([nrm, d[:, None]], axis=1)
+    def plane(ax, ay, bx, by):
+        r1 = Rinv @ np.array([ax, ay, 1]).reshape(3, 1)
+        r2 = Rinv @ np.array([bx, by, 1]).reshape(3, 1)
+        n = np.cross(r1.flatten(), r2.flatten())
+        n /= np.linalg.norm(n)
+        return n[0], n[1], n[2], -np.dot(n, C)
 
-    c = np.arange(proj_w, dtype=np.float64)
-    cx_n = (c - cxp) / fxp
-    col = planes(cx_n, np.full_like(cx_n, (0.0 - cyp) / fyp),
-                 cx_n, np.full_like(cx_n, (proj_h - cyp) / fyp))
-    r = np.arange(proj_h, dtype=np.float64)
-    ry_n = (r - cyp) / fyp
-    row = planes(np.full_like(ry_n, (0.0 - cxp) / fxp), ry_n,
-                 np.full_like(ry_n, (proj_w - cxp) / fxp), ry_n)
+    col = np.zeros((int(proj_w), 4))
+    row = np.zeros((int(proj_h), 4))
+    for c in range(int(proj_w)):            # the column's line from (c, 0) to (c, PH)
+        x = (c - cxp) / fxp
+        col[c, :] = plane(x, (0 - cyp) / fyp, x, (proj_h - cyp) / fyp)
+    for r in range(int(proj_h)):            # the row's line from (0, r) to (PW, r)
+        y = (r - cyp) / fyp
+        row[r, :] = plane((0 - cxp) / fxp, y, (proj_w - cxp) / fxp, y)
     return col, row
 
 

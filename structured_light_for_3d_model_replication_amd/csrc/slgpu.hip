@@ -52,7 +52,10 @@ constexpr int kTileBlock = SLG_TILE_BLOCK;  // main3 workgroup (512 measured slo
 constexpr int kTilePx = kTileBlock * kPx;   // 2048 pixels per main3 tile (one look-back entry)
 constexpr int kMapsPx = kBlock * kPx;       // 2048 pixels per decode_maps workgroup
 constexpr int kMaxBits = 15;                // packed 16-bit code lanes
-constexpr int kLookK = 2;                  // look-back window = 2 x 64 predecessor tiles per poll
+#ifndef SLG_LOOK_K
+#define SLG_LOOK_K 2
+#endif
+constexpr int kLookK = SLG_LOOK_K;         // look-back window = kLookK x 64 predecessor tiles per poll
 constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagInc = 2ull << 62;
 constexpr uint64_t kValMask = (1ull << 62) - 1;
@@ -632,6 +635,8 @@ struct MainParams {
   int32_t div_fast;
   int32_t rays_fast;          // host-verified: every pixel's ray takes the Markstein path (tri_item FAST)
   double o0, o1, o2;
+  int32_t num_pre;            // pcol (and prow in row_mode 2) hold numer in column 3, not d
+  int32_t pad_np;
   const double* pcol;
   int32_t n_pcol;
   const double* prow;
@@ -789,6 +794,8 @@ __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int
   if (RAYS == SLG_RAYS_PINHOLE) {
     // The same IEEE quotients as the reference, with the divisions by fx, fy (per camera)
     // and by the norm (three per pixel) done as Markstein corrections of one reciprocal.
+    // (Per-column / per-row tables of x and y measured 8 % slower: two more L2 gathers per
+    // point cost more than the fp64 they replace.)
     const double ax = double(u) - p.cx, ay = double(v) - p.cy;
     double x, y;
     if constexpr (FAST) {
@@ -811,7 +818,9 @@ __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int
   }
   TriOut o;
   const double den = (pc01.x * r0 + pc01.y * r1) + pc23.x * r2;          // np.sum(N*rays, 0)
-  const double num = ((pc01.x * p.o0 + pc01.y * p.o1) + pc23.x * p.o2) + pc23.y;
+  // numer = n.Oc + d (processing.py:163-165): precomputed per plane by the caller (column 3 of
+  // the table) or computed here
+  const double num = p.num_pre ? pc23.y : ((pc01.x * p.o0 + pc01.y * p.o1) + pc23.x * p.o2) + pc23.y;
   const bool okc = fabs(den) > 1e-6;
   double t;
   if constexpr (FAST) {
@@ -829,7 +838,7 @@ __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int
   }
   if constexpr (ROW_MODE == 2) {                          // independent row cloud, :218-228
     const double dr = (pr01.x * r0 + pr01.y * r1) + pr23.x * r2;
-    const double nr = ((pr01.x * p.o0 + pr01.y * p.o1) + pr23.x * p.o2) + pr23.y;
+    const double nr = p.num_pre ? pr23.y : ((pr01.x * p.o0 + pr01.y * p.o1) + pr23.x * p.o2) + pr23.y;
     const bool okr = fabs(dr) > 1e-6;
     double tr;
     if constexpr (FAST) {
@@ -1019,6 +1028,9 @@ constexpr int kMaxViews = 16;
 #ifndef SLG_DECODE_BATCH
 #define SLG_DECODE_BATCH 11                // pairs per axis in flight per lane (4/6/8/11: 31.7/30.3/28.7/27.5 us/view)
 #endif
+#ifndef SLG_TRI_GROUP
+#define SLG_TRI_GROUP 2                    // phase B: rounds (items per lane) computed per step
+#endif
 #ifndef SLG_M3_WAVES
 #define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
 #endif
@@ -1173,6 +1185,46 @@ __device__ inline int2 block_scan(int x, int* s_wtot) {
   return make_int2(off + incl - x, tot);
 }
 
+// Phase B of main3 for rounds [i, i + G) (item m = tid + 256 * round), FAST path: the G items'
+// loads and fp64 chains are independent, so their plane gathers are in flight together.
+// tri_rounds: i is a compile-time multiple of G (the unrolled group loop); tri_rounds_at: any i.
+template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt>
+__device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, const uint32_t* s_code,
+                                     const uint32_t* s_uv, XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
+  const int tid = threadIdx.x;
+  TriOut o[G];
+  bool in[G];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    const int m = tid + kTileBlock * (i + h);
+    in[h] = m < n_items;
+    const uint32_t sc = s_code[m], suv = s_uv[m];   // m < kTilePx; garbage past n_items masked
+    const uint32_t code = in[h] ? sc : 0u, uv = in[h] ? suv : 0u;
+    o[h] = tri_item<ROW_MODE, RAYS, true>(p, code, int(uv & 0xffffu), int(uv >> 16));
+  }
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    const uint32_t keep = in[h] ? o[h].keep : 0u;
+    // runtime round index: select into the register arrays (unrolled compares, no scratch)
+#pragma unroll
+    for (int r = 0; r < kIt; ++r)
+      if (r == i + h) {
+        pts[0][r][0] = XT(o[h].x); pts[0][r][1] = XT(o[h].y); pts[0][r][2] = XT(o[h].z);
+        if constexpr (ROW_MODE == 2) {
+          pts[NS - 1][r][0] = XT(o[h].rx); pts[NS - 1][r][1] = XT(o[h].ry); pts[NS - 1][r][2] = XT(o[h].rz);
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) km[s][r] = __ballot((keep >> s) & 1u);
+      }
+  }
+}
+
+template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt>
+__device__ inline void tri_rounds(const MainParams& p, int i, int n_items, const uint32_t* s_code,
+                                  const uint32_t* s_uv, XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
+  tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt>(p, i, n_items, s_code, s_uv, pts, km);
+}
+
 // PROF: the profiling instance (SLG_DBG set): honours the ablation bits of MainParams::dbg and
 // writes per-workgroup phase records; the production instances carry none of that code.
 template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS, bool PROF>
@@ -1273,40 +1325,40 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // ~15 VGPRs for a fifth wave per SIMD but measured 6% slower).
   XT pts[NS][kIt][3];
   uint64_t km[NS][kIt];
-  static_assert(kIt % 2 == 0, "paired rounds");
+  static_assert(kIt % SLG_TRI_GROUP == 0, "grouped rounds");
   const bool trivial = PROF && (p.dbg & 2);          // ablation: no triangulation arithmetic
   if (p.rays_fast && !trivial) {
-    // Two rounds per step: two independent straight-line fp64 chains (and their plane
-    // gathers) per lane, so the latency of one hides behind the other.
+    // Several rounds per step: independent straight-line fp64 chains per lane whose plane
+    // gathers (L2, high latency under the streaming load) are all in flight together.  The
+    // tile's round count is block-uniform: full groups of SLG_TRI_GROUP rounds, then a pair,
+    // then a single round, so no empty round is computed.
+    const int rounds = (n_items + kB - 1) / kB;
+    int i = 0;
 #pragma unroll
-    for (int i = 0; i < kIt; i += 2) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) km[s][i] = km[s][i + 1] = 0;
-      if (i * kB < n_items) {                        // block-uniform
-        TriOut o[2];
-        bool in[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int m = tid + kB * (i + h);
-          in[h] = m < n_items;
-          const uint32_t sc = s_code[m], suv = s_uv[m];   // m < kTilePx; garbage past n_items masked
-          const uint32_t code = in[h] ? sc : 0u, uv = in[h] ? suv : 0u;
-          o[h] = tri_item<ROW_MODE, RAYS, true>(p, code, int(uv & 0xffffu), int(uv >> 16));
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t keep = in[h] ? o[h].keep : 0u;
-          pts[0][i + h][0] = XT(o[h].x); pts[0][i + h][1] = XT(o[h].y); pts[0][i + h][2] = XT(o[h].z);
-          if constexpr (ROW_MODE == 2) {
-            pts[NS - 1][i + h][0] = XT(o[h].rx); pts[NS - 1][i + h][1] = XT(o[h].ry); pts[NS - 1][i + h][2] = XT(o[h].rz);
-          }
-#pragma unroll
-          for (int s = 0; s < NS; ++s) km[s][i + h] = __ballot((keep >> s) & 1u);
-        }
+    for (int g = 0; g + SLG_TRI_GROUP <= kIt; g += SLG_TRI_GROUP)
+      if (i + SLG_TRI_GROUP <= rounds) {
+        tri_rounds<SLG_TRI_GROUP, ROW_MODE, RAYS, XT, NS, kIt>(p, g, n_items, s_code, s_uv, pts, km);
+        i = g + SLG_TRI_GROUP;
       }
-      if (lane == 0) {
+    if (SLG_TRI_GROUP > 2 && i + 2 <= rounds) {
+      tri_rounds_at<2, ROW_MODE, RAYS, XT, NS, kIt>(p, i, n_items, s_code, s_uv, pts, km);
+      i += 2;
+    }
+    if (i < rounds) {
+      tri_rounds_at<1, ROW_MODE, RAYS, XT, NS, kIt>(p, i, n_items, s_code, s_uv, pts, km);
+      i += 1;
+    }
 #pragma unroll
-        for (int s = 0; s < NS; ++s) { s_cnt[s][i][wave] = __popcll(km[s][i]); s_cnt[s][i + 1][wave] = __popcll(km[s][i + 1]); }
+    for (int r = 0; r < kIt; ++r)
+      if (r >= i) {
+#pragma unroll
+        for (int s2 = 0; s2 < NS; ++s2) km[s2][r] = 0;
+      }
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 0; r < kIt; ++r) {
+#pragma unroll
+        for (int s2 = 0; s2 < NS; ++s2) s_cnt[s2][r][wave] = __popcll(km[s2][r]);
       }
     }
   } else {
@@ -1624,6 +1676,14 @@ int fill_calib(MainParams& mp, const slg_calib* c, const slg_tri_params* tp, int
   mp.o0 = c->oc[0]; mp.o1 = c->oc[1]; mp.o2 = c->oc[2];
   mp.pcol = c->col_planes; mp.n_pcol = c->n_col_planes;
   mp.prow = c->row_planes; mp.n_prow = c->n_row_planes;
+  // optional per-plane numerators (slg_calib, ABI 2)
+  mp.num_pre = c->col_planes_num && (tp->row_mode != 2 || c->row_planes_num) ? 1 : 0;
+  if (mp.num_pre) {
+    mp.pcol = c->col_planes_num;
+    if (tp->row_mode == 2) mp.prow = c->row_planes_num;
+  }
+  if ((reinterpret_cast<uintptr_t>(c->col_planes_num) | reinterpret_cast<uintptr_t>(c->row_planes_num)) & 15)
+    return fail(SLG_ERR_INVALID, "numerator plane tables must be 16-byte aligned");
   mp.tol = tp->epipolar_tol;
   mp.n_px = n_px;
   mp.width = width;

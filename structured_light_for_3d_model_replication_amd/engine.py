@@ -114,15 +114,28 @@ class DeviceCalib:
     kernels recompute the identical values, saving 24 B per pixel of HBM traffic.
     """
 
-    def __init__(self, calib: dict, height: int, width: int, device=None, keep_table=False):
+    def __init__(self, calib: dict, height: int, width: int, device=None, keep_table=False, tables=True):
         device = device or default_device()
         self.height, self.width = int(height), int(width)
+        self.tables = bool(tables)          # pass the numerator tables (else computed per point)
         K = np.asarray(calib["cam_K"], dtype=np.float64)
         self.fx, self.fy, self.cx, self.cy = float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2])
         self.oc = np.asarray(calib["Oc"], dtype=np.float64).reshape(-1)[:3]
         self.col_planes = torch.from_numpy(_plane_table(calib["wPlaneCol"])).to(device)
         self.row_planes = (torch.from_numpy(_plane_table(calib["wPlaneRow"])).to(device)
                            if "wPlaneRow" in calib and calib["wPlaneRow"] is not None else None)
+        # planes with column 3 = numer = np.dot(N, Oc) + d, the reference's own expression
+        # (processing.py:166,219), evaluated once per plane instead of per point
+        oc = np.zeros((3, 1)) if self.oc.size < 3 else self.oc[:3].reshape(3, 1)
+
+        def with_num(tab):
+            t = _plane_table(tab).copy()
+            t[:, 3] = np.dot(t[:, 0:3], oc).flatten() + t[:, 3]
+            return torch.from_numpy(np.ascontiguousarray(t)).to(device)
+
+        self.col_planes_num = with_num(calib["wPlaneCol"])
+        self.row_planes_num = (with_num(calib["wPlaneRow"])
+                               if "wPlaneRow" in calib and calib["wPlaneRow"] is not None else None)
         Nc = np.asarray(calib["Nc"])
         self.rays = None
         self.ray_mode = N.RAYS_PINHOLE
@@ -149,6 +162,9 @@ class DeviceCalib:
         if self.row_planes is not None:
             c.row_planes = self.row_planes.data_ptr()
             c.n_row_planes = self.row_planes.shape[0]
+        if self.tables:
+            c.col_planes_num = self.col_planes_num.data_ptr()
+            c.row_planes_num = self.row_planes_num.data_ptr() if self.row_planes_num is not None else 0
         return c
 
 

@@ -34,7 +34,7 @@ def test_library_loads_and_exports_every_header_symbol():
     import json
     r = json.loads(out.stdout.strip().splitlines()[-1])
     assert len(header_exports()) >= 9
-    assert r["missing"] == [] and r["v"] == 1
+    assert r["missing"] == [] and r["v"] == 2
     assert len(r["hip"]) == 1, r["hip"]          # one HIP runtime (torch's) in the process
     assert r["ws"] > 1920 * 1080 * 27
 
@@ -44,14 +44,30 @@ def test_exports_match_ctypes_table():
     assert sorted(N.EXPORTS) == header_exports()
 
 
-def test_ctypes_struct_layout_matches_header():
+def test_ctypes_struct_layout_matches_header(tmp_path):
+    """Every ctypes structure has the C compiler's size and field offsets for include/slgpu.h."""
     from structured_light_for_3d_model_replication_amd import _native as N
     import ctypes
-    assert ctypes.sizeof(N.Capture) == 40
-    assert ctypes.sizeof(N.DecodeParams) == 40
-    assert ctypes.sizeof(N.Calib) == 8 + 8 + 32 + 24 + 16 + 16
-    assert ctypes.sizeof(N.TriParams) == 16
-    assert ctypes.sizeof(N.Cloud) == 32
+    structs = {"slg_capture": N.Capture, "slg_decode_params": N.DecodeParams, "slg_calib": N.Calib,
+               "slg_tri_params": N.TriParams, "slg_maps": N.Maps, "slg_cloud": N.Cloud}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/slgpu.h"', 'int main(void) {']
+    for cname, cls in structs.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'  printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("  return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-o", str(exe), str(src)], check=True)
+    want = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        name, field, val = line.split()
+        want[(name, field)] = int(val)
+    for cname, cls in structs.items():
+        assert ctypes.sizeof(cls) == want[(cname, "size")], cname
+        for f, _ in cls._fields_:
+            assert getattr(cls, f).offset == want[(cname, f)], (cname, f)
 
 
 def test_discovery_orders(tmp_path):
@@ -125,9 +141,9 @@ def test_calibration_tables_match_reference_calibrate_final():
     ref = load_calibs()["rig"]
     mine = synth.default_rig(96, 64, 1920, 1080).tables()
     assert np.array_equal(mine["Nc"], ref["Nc"])           # bitwise: pinhole rays
-    for k in ("wPlaneCol", "wPlaneRow"):
+    for k in ("wPlaneCol", "wPlaneRow"):                     # bitwise: stripe planes
         assert mine[k].shape == ref[k].shape
-        np.testing.assert_allclose(mine[k], ref[k], rtol=0, atol=1e-12)
+        assert np.array_equal(mine[k], ref[k]), (k, np.abs(mine[k] - ref[k]).max())
     assert np.array_equal(mine["Oc"], ref["Oc"]) and np.array_equal(mine["cam_K"], ref["cam_K"])
 
 

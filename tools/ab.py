@@ -42,7 +42,7 @@ def worker(a):
     cal = rig.tables()
     dev = torch.device("cuda", 0)
     pool = [E.DeviceFrames(list(frames[i]), tex[i], device=dev) for _ in range(3) for i in range(12)]
-    dcal = E.DeviceCalib(cal, H, W, device=dev)
+    dcal = E.DeviceCalib(cal, H, W, device=dev, tables=a.tables != "none")
     cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
     B = 12
     beng = E.BatchReconstructor(H, W, B, device=dev, slots=2)
@@ -89,19 +89,24 @@ def main():
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--worker", action="store_true")
+    ap.add_argument("--tables", default="num", help="worker: num | none (DeviceCalib numerator tables)")
+    ap.add_argument("--variants", default="", help="comma list of lib[:tables] (overrides --libs)")
     ap.add_argument("--timeout", type=int, default=240)
     a = ap.parse_args()
     if a.worker:
         return worker(a)
-    libs = [x for x in a.libs.split(",") if x] or [""]
+    libs = [x for x in (a.variants or a.libs).split(",") if x] or [""]
     res = {lib: [] for lib in libs}
     ref = None
     for r in range(a.rounds):
         for lib in libs:
             env = dict(os.environ)
-            if lib:
-                env["SLG_LIB"] = lib
+            path, _, opt = lib.partition(":")
+            if path:
+                env["SLG_LIB"] = path
             cmd = [sys.executable, __file__, "--worker", "--launches", str(a.launches), "--warmup", str(a.warmup)]
+            if opt:
+                cmd += ["--tables", opt]
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout)
             if p.returncode != 0:
                 print(f"[ab] {lib} round {r} FAILED rc={p.returncode}\n{p.stderr[-3000:]}", file=sys.stderr, flush=True)
