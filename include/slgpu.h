@@ -226,6 +226,22 @@ int32_t slg_rays_match_pinhole(const double *rays, int32_t height, int32_t width
                                double fy, double cx, double cy, int64_t *mismatches,
                                void *stream);
 
+/* Colour captures (the phone path: canvas PNGs uploaded by frontend/App.tsx:234-247 and saved
+ * as-is by server/server.py:86) on the device, from ONE upload of the decoded frames:
+ * gray[f][i] = cv2.imread(f, 0) of rgb frame f (RGB or RGBA bytes, `channels` 3|4, frame f at
+ * rgb + f * src_stride) into a frame stack of gray_stride, and, when bgr0 is not NULL, frame 0
+ * as the BGR texture cv2.imread(files[0]) returns.  weights: libpng's rgb_to_gray fixed point
+ * (PNG) or OpenCV's BGR2GRAY weights (BMP) -- restated from the libraries' published formulas,
+ * parity unpinned (no OpenCV here).  Replaces the host conversion of frames.py. */
+#define SLG_GRAY_PNG 0
+#define SLG_GRAY_BMP 1
+int32_t slg_rgb_to_gray(const uint8_t *rgb, int32_t channels, int64_t n_pixels, int64_t src_stride,
+                        int32_t n_frames, uint8_t *gray, int64_t gray_stride, uint8_t *bgr0,
+                        int32_t weights, void *stream);
+/* Texture of a gray capture (cv2.imread(files[0]) of an 8-bit gray PNG: frame 0 replicated to
+ * B, G, R) built on the device from the uploaded frame 0: no host replication, no extra upload. */
+int32_t slg_gray_texture(const uint8_t *frame0, int64_t n_pixels, uint8_t *bgr, void *stream);
+
 /* Host: write an ASCII PLY exactly as ProcessingLogic._save_ply does (processing.py:236-248):
  * header, then "%.4f %.4f %.4f R G B" per point (Python's correctly rounded formatting, BGR
  * swapped to RGB).  xyz/bgr are HOST arrays [n][3].  Formats on n_threads host threads

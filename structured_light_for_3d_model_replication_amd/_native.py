@@ -28,6 +28,7 @@ SLG_ERR_INDEX = 5
 THRESH_OTSU, THRESH_MANUAL, THRESH_PERCENTILE = 0, 1, 2
 VARIANT_PROCESSING, VARIANT_SLSYSTEM = 0, 1
 RAYS_TABLE, RAYS_PINHOLE = 0, 1
+GRAY_PNG, GRAY_BMP = 0, 1
 
 c_i32, c_i64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -102,6 +103,8 @@ EXPORTS = {
     "slg_png_gray8_size": (c_i32, [ctypes.c_char_p, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
     "slg_png_gray8_decode": (c_i32, [ctypes.c_char_p, c_vp, c_i64, c_i32, c_i32]),
     "slg_rays_match_pinhole": (c_i32, [c_vp, c_i32, c_i32, c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_vp]),
+    "slg_rgb_to_gray": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp]),
+    "slg_gray_texture": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
     "slg_gather_unique_id": (c_i32, [c_vp]),
     "slg_gather_init": (c_i32, [ctypes.POINTER(c_vp), c_i32, c_i32, c_vp]),
     "slg_gather_counts": (c_i32, [c_vp, c_vp, c_i32, c_vp, c_vp]),

@@ -25,6 +25,7 @@ def main(argv=None):
     ap.add_argument("--thresh", choices=["otsu", "manual"], default="otsu")
     ap.add_argument("--shadow-val", type=float, default=40)
     ap.add_argument("--contrast-val", type=float, default=10)
+    ap.add_argument("--batch-views", type=int, default=8, help="views per batched GPU launch (1..16)")
     a = ap.parse_args(argv)
 
     import torch
@@ -41,7 +42,8 @@ def main(argv=None):
                                 row_mode=a.row_mode, epipolar_tol=a.epipolar_tol,
                                 thresh_mode=a.thresh,
                                 shadow_val=int(a.shadow_val) if a.shadow_val.is_integer() else a.shadow_val,
-                                contrast_val=int(a.contrast_val) if a.contrast_val.is_integer() else a.contrast_val)
+                                contrast_val=int(a.contrast_val) if a.contrast_val.is_integer() else a.contrast_val,
+                                batch_views=a.batch_views)
     finally:
         if world > 1:
             dist.destroy_process_group()

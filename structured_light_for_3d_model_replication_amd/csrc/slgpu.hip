@@ -1493,6 +1493,52 @@ __global__ __launch_bounds__(kBlock) void row_tail_kernel(WsHeader* ws, const vo
   }
 }
 
+// Colour captures (the reference's phone path uploads canvas PNGs, frontend/App.tsx:234-247,
+// saved as-is by server/server.py:86): cv2.imread(f, 0) turns each frame to gray and
+// cv2.imread(files[0]) gives frame 0 as BGR.  One upload of the decoded RGB(A) frames feeds
+// both: gray planes into the frame stack (libpng's rgb_to_gray 15-bit fixed point for PNG,
+// OpenCV's BGR2GRAY 14-bit weights for BMP -- restated, parity unpinned) and frame 0's BGR
+// texture.  16 pixels per lane: channel bytes are read as 16 x C contiguous bytes.
+constexpr int kRgbPx = 16;
+__global__ __launch_bounds__(kBlock) void rgb_gray_kernel(const uint8_t* rgb, int32_t channels, int64_t n_px,
+                                                          int64_t src_stride, uint8_t* gray, int64_t gray_stride,
+                                                          uint8_t* bgr0, int32_t bmp) {
+  const int f = blockIdx.y;
+  const int64_t px0 = (int64_t(blockIdx.x) * kBlock + threadIdx.x) * kRgbPx;
+  if (px0 >= n_px) return;
+  const uint8_t* src = rgb + int64_t(f) * src_stride + px0 * channels;
+  uint8_t* dst = gray + int64_t(f) * gray_stride + px0;
+  const int n = n_px - px0 < kRgbPx ? int(n_px - px0) : kRgbPx;
+  uint32_t g4[kRgbPx / 4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < kRgbPx; ++k) {
+    if (k >= n) break;
+    const uint32_t r = src[k * channels], g = src[k * channels + 1], b = src[k * channels + 2];
+    const uint32_t y = bmp ? (b * 1868u + g * 9617u + r * 4899u + 8192u) >> 14
+                           : (r * 9797u + g * 19234u + b * 3737u + 16384u) >> 15;
+    g4[k >> 2] |= (y & 0xffu) << (8 * (k & 3));
+    if (bgr0 && f == 0) {
+      bgr0[(px0 + k) * 3] = uint8_t(b);
+      bgr0[(px0 + k) * 3 + 1] = uint8_t(g);
+      bgr0[(px0 + k) * 3 + 2] = uint8_t(r);
+    }
+  }
+  if (n == kRgbPx && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    *reinterpret_cast<uint4*>(dst) = make_uint4(g4[0], g4[1], g4[2], g4[3]);
+  } else {
+    for (int k = 0; k < n; ++k) dst[k] = uint8_t(g4[k >> 2] >> (8 * (k & 3)));
+  }
+}
+
+// Gray frame stack whose texture is frame 0 replicated (cv2.imread(f) of an 8-bit gray PNG):
+// bgr[i] = (g, g, g) with g = frame0[i].
+__global__ __launch_bounds__(kBlock) void gray_texture_kernel(const uint8_t* frame0, int64_t n_px, uint8_t* bgr) {
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n_px) return;
+  const uint8_t g = frame0[i];
+  bgr[3 * i] = g; bgr[3 * i + 1] = g; bgr[3 * i + 2] = g;
+}
+
 __global__ __launch_bounds__(kBlock) void pinhole_kernel(const double* rays, int64_t n_px, int width, double fx,
                                                          double fy, double cx, double cy,
                                                          unsigned long long* mismatches) {
@@ -2198,6 +2244,27 @@ int32_t slg_decode_stats_partials_batch(int32_t n_views, int32_t height, int32_t
     if (rc) return rc;
   }
   return SLG_OK;
+}
+
+int32_t slg_rgb_to_gray(const uint8_t* rgb, int32_t channels, int64_t n_pixels, int64_t src_stride, int32_t n_frames,
+                        uint8_t* gray, int64_t gray_stride, uint8_t* bgr0, int32_t weights, void* stream) {
+  if (!rgb || !gray || n_pixels < 1 || n_frames < 1 || (channels != 3 && channels != 4))
+    return fail(SLG_ERR_INVALID, "bad rgb_to_gray argument");
+  if (src_stride < n_pixels * channels || gray_stride < n_pixels)
+    return fail(SLG_ERR_INVALID, "strides smaller than a frame");
+  if (weights != SLG_GRAY_PNG && weights != SLG_GRAY_BMP) return fail(SLG_ERR_INVALID, "bad weights");
+  const int64_t per_block = int64_t(kBlock) * kRgbPx;
+  hipLaunchKernelGGL(rgb_gray_kernel, dim3(unsigned((n_pixels + per_block - 1) / per_block), unsigned(n_frames)),
+                     dim3(kBlock), 0, static_cast<hipStream_t>(stream), rgb, channels, n_pixels, src_stride, gray,
+                     gray_stride, bgr0, weights == SLG_GRAY_BMP ? 1 : 0);
+  return check_launch("rgb_gray_kernel");
+}
+
+int32_t slg_gray_texture(const uint8_t* frame0, int64_t n_pixels, uint8_t* bgr, void* stream) {
+  if (!frame0 || !bgr || n_pixels < 1) return fail(SLG_ERR_INVALID, "bad gray_texture argument");
+  hipLaunchKernelGGL(gray_texture_kernel, dim3(unsigned((n_pixels + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), frame0, n_pixels, bgr);
+  return check_launch("gray_texture_kernel");
 }
 
 int32_t slg_rays_match_pinhole(const double* rays, int32_t height, int32_t width, double fx, double fy, double cx,

@@ -192,8 +192,8 @@ def process_batch_sharded(calib_path, target_path, log_callback=None, process_so
     folders = view_folders(target_path)
     mine = shard(folders, rank, world)
     if process_source is None:
-        # the single-process batch pipeline (prefetch read, GPU, writer thread) on this
-        # rank's block of folders
+        # the single-process batch pipeline (pinned reads ahead, batched launches, writer
+        # thread) on this rank's block of folders
         import scipy.io
         from . import engine as E
         data = scipy.io.loadmat(calib_path)
@@ -201,10 +201,9 @@ def process_batch_sharded(calib_path, target_path, log_callback=None, process_so
         cfg_kw = {k: kw[k] for k in ("n_sets_col", "n_sets_row", "thresh_mode", "shadow_val",
                                      "contrast_val") if k in kw}
         cfg = E.DecodeConfig(1920, 1080, **cfg_kw)
-        ok = PR.run_view_folders(
-            mine, log, PR.batch_reconstruct_stage(cfg, calib, kw.get("row_mode", 1),
-                                                  kw.get("epipolar_tol", 2.0), log),
-            read=lambda f: PR.read_capture(f, cfg), write=PR.batch_write_stage())
+        from .pipeline import BatchPipeline
+        ok = BatchPipeline(cfg, calib, kw.get("row_mode", 1), kw.get("epipolar_tol", 2.0),
+                           group=kw.get("batch_views", PR.batch_views()), log=log).run(mine, PR.batch_write_stage())
     else:
         def one(folder, _host):
             name = os.path.basename(folder) + ".ply"

@@ -91,6 +91,19 @@ class DeviceFrames:
             tex = np.ascontiguousarray(texture, dtype=np.uint8).reshape(self.n_px, 3)
             self.texture = torch.from_numpy(tex).to(device)
 
+    @classmethod
+    def allocate(cls, n_frames: int, height: int, width: int, device=None) -> "DeviceFrames":
+        """Uninitialised stack + texture of this layout, for a caller that fills them itself
+        (the batch file pipeline: async H2D from pinned host memory, device-side texture)."""
+        self = cls.__new__(cls)
+        device = device or default_device()
+        self.height, self.width, self.n_px = int(height), int(width), int(height) * int(width)
+        self.n_frames = int(n_frames)
+        self.stride = (self.n_px + 15) // 16 * 16
+        self.data = torch.empty((max(self.n_frames, 2), self.stride), dtype=torch.uint8, device=device)
+        self.texture = torch.empty((self.n_px, 3), dtype=torch.uint8, device=device)
+        return self
+
     def capture(self) -> N.Capture:
         return N.Capture(frames=self.data.data_ptr(), frame_stride=self.stride,
                          n_frames=self.n_frames, height=self.height, width=self.width,

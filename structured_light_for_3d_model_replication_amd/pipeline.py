@@ -1,0 +1,343 @@
+"""Batch mode over view folders as a host/GPU pipeline (``process_multi_ply(mode='batch')``,
+``server/processing.py:314-334``; the auto-scan layout of ``server/gui.py:1718,1753``).
+
+The reference loops over the view folders one by one: read 40-odd PNGs, decode, triangulate,
+write an ASCII PLY.  Here the same work is a pipeline whose stages overlap:
+
+* **read** (thread pool, up to ``depth`` folders ahead): discover the files, decode the frames the
+  decode needs straight into a **pinned** host frame stack (native 8-bit gray PNG decoder into the
+  stack rows; colour frames into a pinned RGB(A) stack, converted on the device);
+* **upload** (copy stream): async H2D of a group of up to ``group`` views;
+* **reconstruct** (compute stream): device texture (frame 0 replicated, or frame 0's BGR from the
+  colour upload), then ONE batched stats launch + ONE fused decode/triangulate launch for the
+  group (``BatchReconstructor.run``, ``slg_reconstruct_batch``) -- launched before the previous
+  group is collected, so uploads and kernels of consecutive groups overlap;
+* **collect**: counts, D2H of the float64 clouds into pinned buffers;
+* **write** (writer thread): ``slg_ply_write`` (byte-identical ASCII PLY).
+
+Per-folder behaviour is the reference's: folders without images are skipped with its message,
+an exception in any stage of one folder is logged as ``❌ Error in <folder>: <msg>`` and the loop
+goes on (a failing group launch falls back to one view at a time to find the culprit), and the
+progress lines of each folder come out in folder order, each folder's ``✔ Saved`` after its
+``-> Saving`` line.  Returns the number of folders that succeeded.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import engine as E
+from . import frames as FR
+
+
+class PinnedPool:
+    """Reusable page-locked host buffers (cudaHostAlloc is slow; a batch reuses a few sizes)."""
+
+    def __init__(self):
+        self._free: dict[int, list] = {}
+
+    def get(self, nbytes: int) -> torch.Tensor:
+        lst = self._free.get(nbytes)
+        if lst:
+            return lst.pop()
+        return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+
+    def put(self, t: torch.Tensor | None):
+        if t is not None:
+            self._free.setdefault(t.numel(), []).append(t)
+
+
+@dataclass
+class HostView:
+    """One view folder read into pinned host memory."""
+    folder: str
+    n_files: int
+    height: int
+    width: int
+    stride: int
+    kind: str                       # "gray": stack holds gray frames; "rgb": RGB(A) frames
+    stack: torch.Tensor             # pinned uint8 [F, stride] (gray) or [F, n_px * channels] (rgb)
+    channels: int = 1
+    weights: int = N.GRAY_PNG       # rgb: libpng (PNG) or OpenCV (BMP) gray weights
+    texture: torch.Tensor | None = None   # pinned [n_px, 3] BGR, or None: derived on the device
+    pinned: list = field(default_factory=list)   # buffers to return to the pool
+
+
+def _decode_rgb(path) -> np.ndarray:
+    """Decoded colour frame as RGB or RGBA bytes [H, W, C] (8-bit), for the device conversion."""
+    im = FR._open(path)
+    if im is None:
+        raise AttributeError("'NoneType' object has no attribute 'astype'")
+    a = np.asarray(im)
+    if a.dtype == np.uint16:
+        a = (a >> 8).astype(np.uint8)
+    return a
+
+
+def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", "png")) -> HostView:
+    """Discover + decode one capture into pinned memory (host work only; safe on any thread)."""
+    from .processing import _needed_frames
+    files = FR.discover(folder, order)
+    if len(files) < 4:
+        raise ValueError(f"Not enough images (got {len(files)}, need at least 4).")
+    need = _needed_frames(len(files), cfg) if cfg.variant == "processing" else list(range(len(files)))
+    L = N.lib()
+    w, h = ctypes.c_int32(), ctypes.c_int32()
+    gray8 = (files[0].lower().endswith(".png") and not os.environ.get("SLG_PNG_PIL")
+             and L.slg_png_gray8_size(os.fsencode(files[0]), ctypes.byref(w), ctypes.byref(h)) == 0)
+    workers = min(FR.decode_threads(), len(need))
+    if gray8:
+        H, W = h.value, w.value
+        n_px = H * W
+        stride = (n_px + 15) // 16 * 16
+        buf = pool.get(len(files) * stride)
+        stack = buf.view(len(files), stride)
+        base = stack.data_ptr()
+
+        def one(i):
+            p = files[i]
+            dst = base + i * stride
+            if L.slg_png_gray8_decode(os.fsencode(p), ctypes.c_void_p(dst), n_px, W, H) == 0:
+                return
+            a = FR.imread_gray(p)                   # any other file: the general decoder
+            if a.shape != (H, W):
+                raise ValueError("all frames must have the same size")
+            stack[i, :n_px].copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1)))
+        with ThreadPoolExecutor(max_workers=workers) as ex:
+            list(ex.map(one, need))
+        return HostView(folder, len(files), H, W, stride, "gray", stack, pinned=[buf])
+    # colour (or non-PNG) captures: decoded RGB(A) frames, converted to gray on the device
+    first = _decode_rgb(files[0])
+    if first.ndim == 2:                               # a gray file the fast path does not take
+        imgs, tex = FR.load_frames(files, need, texture=True)
+        H, W = imgs[0].shape
+        n_px = H * W
+        stride = (n_px + 15) // 16 * 16
+        buf = pool.get(len(files) * stride)
+        stack = buf.view(len(files), stride)
+        for i, a in zip(need, imgs):
+            if a.shape != (H, W):
+                raise ValueError("all frames must have the same size")
+            stack[i, :n_px].copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1)))
+        tbuf = pool.get(n_px * 3)
+        tbuf.view(n_px, 3).copy_(torch.from_numpy(np.ascontiguousarray(tex).reshape(n_px, 3)))
+        return HostView(folder, len(files), H, W, stride, "gray", stack, texture=tbuf.view(n_px, 3),
+                        pinned=[buf, tbuf])
+    H, W, C = first.shape[0], first.shape[1], min(first.shape[2], 4)
+    if C < 3:
+        raise ValueError(f"unsupported image layout {first.shape}")
+    n_px = H * W
+    buf = pool.get(len(files) * n_px * C)
+    stack = buf.view(len(files), n_px * C)
+
+    def one(i):
+        a = first if i == 0 else _decode_rgb(files[i])
+        if a.ndim != 3 or a.shape[0] != H or a.shape[1] != W or min(a.shape[2], 4) != C:
+            raise ValueError("all frames must have the same size and layout")
+        stack[i].copy_(torch.from_numpy(np.ascontiguousarray(a[..., :C]).reshape(-1)))
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        list(ex.map(one, need))
+    weights = N.GRAY_BMP if files[0].lower().endswith(".bmp") else N.GRAY_PNG
+    return HostView(folder, len(files), H, W, (n_px + 15) // 16 * 16, "rgb", stack, channels=C,
+                    weights=weights, pinned=[buf])
+
+
+def upload_view(hv: HostView, stream, need=None) -> E.DeviceFrames:
+    """Async H2D of a HostView on ``stream`` (pinned source) + the device texture: frame 0
+    replicated for gray captures, frame 0's BGR for colour ones (``slg_gray_texture`` /
+    ``slg_rgb_to_gray``).  The host buffers must stay alive until ``stream`` reaches here."""
+    dev = E.DeviceFrames.allocate(hv.n_files, hv.height, hv.width)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    L = N.lib()
+    with torch.cuda.stream(stream):
+        if hv.kind == "gray":
+            dev.data[: hv.n_files].copy_(hv.stack, non_blocking=True)
+            if hv.texture is not None:
+                dev.texture.copy_(hv.texture, non_blocking=True)
+            else:
+                N.check(L.slg_gray_texture(ctypes.c_void_p(dev.data.data_ptr()), dev.n_px,
+                                           ctypes.c_void_p(dev.texture.data_ptr()), sp))
+        else:
+            rgb = torch.empty(hv.stack.shape, dtype=torch.uint8, device=dev.data.device)
+            rgb.copy_(hv.stack, non_blocking=True)
+            N.check(L.slg_rgb_to_gray(ctypes.c_void_p(rgb.data_ptr()), hv.channels, dev.n_px,
+                                      rgb.shape[1], hv.n_files, ctypes.c_void_p(dev.data.data_ptr()),
+                                      dev.stride, ctypes.c_void_p(dev.texture.data_ptr()), hv.weights, sp))
+            dev._rgb = rgb                              # keep the staging alive with the frames
+    return dev
+
+
+@dataclass
+class _Group:
+    entries: list                   # [(folder, future | None)] in folder order (None: skipped)
+    views: list = field(default_factory=list)   # [(index in entries, HostView, DeviceFrames)]
+    errors: dict = field(default_factory=dict)  # entry index -> exception
+    event: object = None
+    batch: object = None
+    clouds: list = field(default_factory=list)
+
+
+class BatchPipeline:
+    """The pipeline of this module's docstring for one decode configuration + calibration."""
+
+    def __init__(self, cfg: E.DecodeConfig, calib: dict, row_mode=1, epipolar_tol=2.0, group: int = 8,
+                 depth: int | None = None, log=print, order=("bmp", "png")):
+        if row_mode not in (0, 1, 2):
+            raise ValueError("row_mode must be 0, 1 or 2")
+        self.cfg, self.calib, self.row_mode, self.tol = cfg, calib, int(row_mode), float(epipolar_tol)
+        self.group = max(1, min(int(group), E.MAX_VIEWS_PER_LAUNCH))
+        self.depth = depth or 2 * self.group
+        self.log, self.order = log, order
+        self.pool = PinnedPool()
+        self.copy_stream = torch.cuda.Stream()
+        self.compute_stream = torch.cuda.Stream()
+        self.engines: dict = {}
+        self.tables: dict = {}
+        self._slot = 0
+
+    def _engine(self, h, w):
+        key = (h, w)
+        if key not in self.engines:
+            beng = E.BatchReconstructor(h, w, self.group, slots=2)
+            clouds = [[E.Cloud(h * w, self.row_mode, True) for _ in range(self.group)] for _ in range(2)]
+            self.engines[key] = (beng, clouds)
+            self.tables[key] = E.DeviceCalib(self.calib, h, w)
+        return self.engines[key], self.tables[key]
+
+    # ---- stages
+    def _launch(self, g: _Group):
+        """Upload g's views (copy stream) and launch their reconstruction (compute stream)."""
+        for k, (folder, fut) in enumerate(g.entries):
+            if fut is None:
+                continue
+            try:
+                hv = fut.result()
+                g.views.append((k, hv, upload_view(hv, self.copy_stream)))
+            except Exception as e:  # noqa: BLE001 - per-folder isolation like the reference
+                g.errors[k] = e
+        if not g.views:
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.copy_stream)
+        self.compute_stream.wait_event(ev)
+        shapes = {(d.height, d.width) for _, _, d in g.views}
+        slot = self._slot
+        self._slot ^= 1
+        try:
+            if len(shapes) != 1:
+                raise ValueError("views of different sizes")
+            (beng, clouds), dc = self._engine(*shapes.pop())
+            outs = clouds[slot][: len(g.views)]
+            g.batch = beng.prepare([d for _, _, d in g.views], self.cfg, dc, outs, self.row_mode, self.tol, slot=slot)
+            beng.run(g.batch, stream=self.compute_stream)
+            g.clouds = outs
+        except Exception:  # noqa: BLE001 - the group falls back to one view at a time
+            g.batch = None
+        g.event = torch.cuda.Event()
+        g.event.record(self.compute_stream)
+
+    def _collect(self, g: _Group):
+        """Results of g's views as host (P float64 [N,3], C uint8 [N,3]) or exceptions."""
+        res = {}
+        if not g.views:
+            return res
+        g.event.synchronize()
+        if g.batch is not None:
+            for (k, hv, _), c in zip(g.views, g.clouds):
+                n = int(c.count.item())
+                res[k] = (c.xyz[:n].cpu().numpy(), c.bgr[:n].cpu().numpy())
+        else:                                       # isolate the failing view(s)
+            from .processing import reconstruct_view
+            for k, hv, dev in g.views:
+                try:
+                    (_, _), dc = self._engine(dev.height, dev.width)
+                    res[k] = reconstruct_view(dev, self.cfg, self.calib, self.row_mode, self.tol, dc=dc)
+                except Exception as e:  # noqa: BLE001
+                    res[k] = e
+        for _, hv, _ in g.views:                    # uploads are complete: recycle the host buffers
+            for t in hv.pinned:
+                self.pool.put(t)
+        return res
+
+    def run(self, subfolders, write) -> int:
+        """Process ``subfolders`` in order; ``write(folder, (P, C)) -> output name``."""
+        from .processing import has_images
+        log = self.log
+        entries = [(f, has_images(f)) for f in subfolders]
+        success = 0
+        with ThreadPoolExecutor(max_workers=2) as reader, ThreadPoolExecutor(max_workers=1) as writer:
+            futs = {}
+            order = [f for f, ok in entries if ok]
+            nxt = 0
+
+            def prefetch(upto):
+                nonlocal nxt
+                while nxt < len(order) and nxt < upto:
+                    futs[order[nxt]] = reader.submit(read_view, order[nxt], self.cfg, self.pool, self.order)
+                    nxt += 1
+
+            # groups: consecutive entries holding up to `group` folders with images
+            groups, cur, n_img = [], [], 0
+            for f, ok in entries:
+                cur.append((f, ok))
+                n_img += ok
+                if n_img == self.group:
+                    groups.append(cur)
+                    cur, n_img = [], 0
+            if cur:
+                groups.append(cur)
+            done_imgs = 0
+            prefetch(self.depth)
+            prev = None
+            for gi, ents in enumerate(groups + [None]):
+                g = None
+                if ents is not None:
+                    g = _Group([(f, futs.pop(f) if ok else None) for f, ok in ents])
+                    self._launch(g)
+                if prev is not None:
+                    res = self._collect(prev)
+                    done_imgs += sum(1 for _, fut in prev.entries if fut is not None)
+                    prefetch(done_imgs + self.depth)
+                    success += self._report(prev, res, write, writer)
+                prev = g
+        return success
+
+    def _report(self, g: _Group, res, write, writer) -> int:
+        """The group's PLYs written (writer thread, in order) and its log lines in exactly the
+        reference's order per folder: Decoding, then Reconstructing / Saving / ✔ Saved, or the
+        ❌ Error line.  Returns the folders that succeeded."""
+        log, ok, cfg = self.log, 0, self.cfg
+        outcome = {}
+        for k, (folder, fut) in enumerate(g.entries):          # start every write first
+            if fut is None:
+                continue
+            err = g.errors.get(k)
+            r = res.get(k) if err is None else None
+            if err is None and isinstance(r, Exception):
+                err = r
+            outcome[k] = (r, None if err is not None else writer.submit(write, folder, r), err)
+        for k, (folder, fut) in enumerate(g.entries):
+            name = os.path.basename(folder)
+            if fut is None:
+                log(f"  Skipping {name} (No images found).")
+                continue
+            log(f"  -> Decoding folder '{name}'  [col-sets={cfg.n_sets_col}  row-sets={cfg.n_sets_row}]...")
+            r, wf, err = outcome[k]
+            if err is None:
+                log("  -> Reconstructing 3D points...")
+                log(f"  -> Saving {len(r[0])} points...")
+                try:
+                    out = wf.result()
+                    ok += 1
+                    log(f"  ✔ Saved: {out}\n")
+                    continue
+                except Exception as e:  # noqa: BLE001
+                    err = e
+            log(f"  ❌ Error in {name}: {err}\n")
+        return ok

@@ -6,21 +6,6 @@ from __future__ import annotations
 
 import numpy as np
 
-HEADER = ("ply\nformat ascii 1.0\nelement vertex {n}\n"
-          "property float x\nproperty float y\nproperty float z\n"
-          "property uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n")
-
-
-def format_ascii(points, colors) -> str:
-    """The file body as a string (Python's correctly rounded ``%.4f``)."""
-    P = np.asarray(points, dtype=np.float64).reshape(-1, 3)
-    C = np.asarray(colors).reshape(-1, 3)
-    rows = zip(P[:, 0].tolist(), P[:, 1].tolist(), P[:, 2].tolist(),
-               C[:, 2].tolist(), C[:, 1].tolist(), C[:, 0].tolist())
-    return HEADER.format(n=len(P)) + "".join(
-        "%.4f %.4f %.4f %d %d %d\n" % r for r in rows)
-
-
 def write_ascii(filename, points, colors, threads: int = 0) -> None:
     """Write the PLY with the native multithreaded formatter (``slg_ply_write``)."""
     import ctypes

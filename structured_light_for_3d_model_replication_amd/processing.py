@@ -281,13 +281,22 @@ class ProcessingLogic:
             subfolders = [f.path for f in os.scandir(target_path) if f.is_dir()]
             log(f"Found {len(subfolders)} subfolders to process.")
 
-            # Pipelined: the next folder's frames are read on a prefetch thread and this
-            # folder's PLY is written on a writer thread while the following one is
-            # reconstructed (run_view_folders); errors stay per folder as in the reference.
-            success_count = run_view_folders(
-                subfolders, log, batch_reconstruct_stage(cfg, calib_data, row_mode, epipolar_tol, log),
-                read=lambda f: read_capture(f, cfg), write=batch_write_stage())
+            # A host/GPU pipeline (pipeline.BatchPipeline): frames decoded ahead into pinned
+            # memory, groups of views uploaded asynchronously and reconstructed by one batched
+            # launch, PLYs written on a writer thread; per-folder errors and log lines as in
+            # the reference.
+            from .pipeline import BatchPipeline
+            success_count = BatchPipeline(cfg, calib_data, row_mode, epipolar_tol, group=batch_views(),
+                                          log=log).run(subfolders, batch_write_stage())
             log(f"=== Batch Complete: {success_count}/{len(subfolders)} succeeded ===")
+
+
+def batch_views() -> int:
+    """Views per batched launch in batch mode: ``SLG_BATCH_VIEWS`` (1..16), default 8."""
+    try:
+        return max(1, min(16, int(os.environ.get("SLG_BATCH_VIEWS", "8"))))
+    except ValueError:
+        return 8
 
 
 def batch_reconstruct_stage(cfg, calib, row_mode, epipolar_tol, log):

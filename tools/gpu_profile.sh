@@ -10,7 +10,7 @@ BA=${BENCH_ARGS:-}          # e.g. BENCH_ARGS="--config c4" (word-split on purpo
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 echo "[prof] bench" && timeout -k 10 300 python "$R/bench.py" $BA --steps "$STEPS" --warmup 10 > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1
-echo "[prof] kernel trace" && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv -- python "$R/bench.py" $BA --steps ${TRACE_STEPS:-200} --warmup 10 --no-cpu-baseline > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit 2
+echo "[prof] kernel trace" && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv -- python "$R/bench.py" $BA --steps ${TRACE_STEPS:-200} --warmup 10 --no-cpu-baseline --no-verify > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit 2
 echo "[prof] pmc fetch" && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- python "$R/bench.py" $BA --steps ${PMC_STEPS:-24} --warmup 6 --no-verify --no-cpu-baseline > /dev/null 2> "$OUT/fetch.err" || exit 3
 echo "[prof] pmc write" && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- python "$R/bench.py" $BA --steps ${PMC_STEPS:-24} --warmup 6 --no-verify --no-cpu-baseline > /dev/null 2> "$OUT/write.err" || exit 4
 echo "[prof] done"

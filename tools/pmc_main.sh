@@ -1,5 +1,6 @@
 #!/bin/bash
-# PMC passes over the batched fused kernel (kbench main3_batch12), one rocprofv3 run per pass.
+# SQ counter passes over the production fused launches (bench.py's C2 pipeline), one rocprofv3
+# run per pass (each pass within the per-block counter limits).
 # Usage (GPU box, repo root): bash tools/pmc_main.sh <tag>
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -13,6 +14,6 @@ n=0
 for P in "$P1" "$P2" "$P3"; do
   n=$((n+1))
   echo "[pmc] pass $n"
-  timeout -s KILL 150 rocprofv3 --pmc $P -d "$OUT/p$n" -o p$n --output-format csv -- python "$R/tools/kbench.py" --iters 8 --only main3_batch12 > /dev/null 2> "$OUT/p$n.err" || exit $n
+  timeout -s KILL 150 rocprofv3 --pmc $P -d "$OUT/p$n" -o p$n --output-format csv -- python "$R/bench.py" --steps 24 --warmup 4 --settle-ms 0 --no-verify --no-cpu-baseline > /dev/null 2> "$OUT/p$n.err" || exit $n
 done
 echo "[pmc] done"
