@@ -25,7 +25,7 @@ def main(argv=None):
     ap.add_argument("--thresh", choices=["otsu", "manual"], default="otsu")
     ap.add_argument("--shadow-val", type=float, default=40)
     ap.add_argument("--contrast-val", type=float, default=10)
-    ap.add_argument("--batch-views", type=int, default=8, help="views per batched GPU launch (1..16)")
+    ap.add_argument("--batch-views", type=int, default=1, help="views per batched GPU launch (1..16)")
     a = ap.parse_args(argv)
 
     import torch

@@ -108,7 +108,7 @@ def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", 
             a = FR.imread_gray(p)                   # any other file: the general decoder
             if a.shape != (H, W):
                 raise ValueError("all frames must have the same size")
-            stack[i, :n_px].copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1)))
+            stack[i, :n_px].numpy()[:] = a.reshape(-1)
         with ThreadPoolExecutor(max_workers=workers) as ex:
             list(ex.map(one, need))
         return HostView(folder, len(files), H, W, stride, "gray", stack, pinned=[buf])
@@ -124,9 +124,9 @@ def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", 
         for i, a in zip(need, imgs):
             if a.shape != (H, W):
                 raise ValueError("all frames must have the same size")
-            stack[i, :n_px].copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1)))
+            stack[i, :n_px].numpy()[:] = a.reshape(-1)
         tbuf = pool.get(n_px * 3)
-        tbuf.view(n_px, 3).copy_(torch.from_numpy(np.ascontiguousarray(tex).reshape(n_px, 3)))
+        tbuf.view(n_px, 3).numpy()[:] = tex.reshape(n_px, 3)
         return HostView(folder, len(files), H, W, stride, "gray", stack, texture=tbuf.view(n_px, 3),
                         pinned=[buf, tbuf])
     H, W, C = first.shape[0], first.shape[1], min(first.shape[2], 4)
@@ -140,7 +140,7 @@ def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", 
         a = first if i == 0 else _decode_rgb(files[i])
         if a.ndim != 3 or a.shape[0] != H or a.shape[1] != W or min(a.shape[2], 4) != C:
             raise ValueError("all frames must have the same size and layout")
-        stack[i].copy_(torch.from_numpy(np.ascontiguousarray(a[..., :C]).reshape(-1)))
+        stack[i].numpy()[:] = a[..., :C].reshape(-1)          # pinned host tensor: plain memcpy
     with ThreadPoolExecutor(max_workers=workers) as ex:
         list(ex.map(one, need))
     weights = N.GRAY_BMP if files[0].lower().endswith(".bmp") else N.GRAY_PNG

@@ -292,11 +292,15 @@ class ProcessingLogic:
 
 
 def batch_views() -> int:
-    """Views per batched launch in batch mode: ``SLG_BATCH_VIEWS`` (1..16), default 8."""
+    """Views per batched launch in batch mode: ``SLG_BATCH_VIEWS`` (1..16), default 1.  The file
+    path is bound by host PNG decode and PLY formatting, not by the GPU (11 ms of 27 per C2
+    view): a group of 8 waits for 8 reads before its launch and measured 0.050 s/view against
+    0.0275 for 1 over 16 views (profiles/r2k/e2e_files.json); groups pay off for in-memory
+    sources (BatchReconstructor, bench.py)."""
     try:
-        return max(1, min(16, int(os.environ.get("SLG_BATCH_VIEWS", "8"))))
+        return max(1, min(16, int(os.environ.get("SLG_BATCH_VIEWS", "1"))))
     except ValueError:
-        return 8
+        return 1
 
 
 def batch_reconstruct_stage(cfg, calib, row_mode, epipolar_tol, log):

@@ -21,7 +21,8 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--views", type=int, default=6)
+    ap.add_argument("--views", type=int, default=16)
+    ap.add_argument("--groups", type=int, nargs="+", default=[1, 8])
     args = ap.parse_args()
 
     from structured_light_for_3d_model_replication_amd import calibration, synth
@@ -38,29 +39,40 @@ def main():
         folders = sorted(os.path.join(root, d) for d in os.listdir(root))
         kw = dict(n_sets_col=11, n_sets_row=10)
         PR.ProcessingLogic.process_multi_ply(calib, folders[0], "single", log_callback=lambda m: None, **kw)  # warm-up
-        t0 = time.perf_counter()
-        PR.ProcessingLogic.process_multi_ply(calib, root, "batch", log_callback=lambda m: None, **kw)
-        batch_s = (time.perf_counter() - t0) / args.views
+        batch_s = {}
+        for g in args.groups:                        # views per batched launch (SLG_BATCH_VIEWS)
+            os.environ["SLG_BATCH_VIEWS"] = str(g)
+            t0 = time.perf_counter()
+            PR.ProcessingLogic.process_multi_ply(calib, root, "batch", log_callback=lambda m: None, **kw)
+            batch_s[g] = round((time.perf_counter() - t0) / args.views, 4)
 
+        # the pipeline's stages one view at a time, serially (what the overlap hides)
+        import torch
+        from structured_light_for_3d_model_replication_amd import pipeline as PL
         cfg = PR.E.DecodeConfig(1920, 1080, 11, 10, "otsu")
         cal = calibration.load_mat(calib)
+        pool = PL.PinnedPool()
+        s = torch.cuda.Stream()
         t_read = t_rec = t_ply = 0.0
         pts = 0
         for f in folders:
-            t = time.perf_counter(); host = PR.read_capture(f, cfg); t_read += time.perf_counter() - t
+            t = time.perf_counter(); hv = PL.read_view(f, cfg, pool); t_read += time.perf_counter() - t
             t = time.perf_counter()
-            dev, _ = PR.load_capture(f, cfg, host=host)
+            dev = PL.upload_view(hv, s)
+            s.synchronize()
             P, C = PR.reconstruct_view(dev, cfg, cal, 1, 2.0)
             t_rec += time.perf_counter() - t
+            for b in hv.pinned:
+                pool.put(b)
             t = time.perf_counter(); PR.ProcessingLogic._save_ply(P, C, os.path.join(tmp, "x.ply")); t_ply += time.perf_counter() - t
             pts += len(P)
         n = len(folders)
         print(json.dumps({"what": "process_multi_ply batch, C2 PNG folders (end to end)", "views": n,
-                          "points_per_view": pts // n, "s_per_view_batch": round(batch_s, 4),
-                          "s_per_view_parts": {"read_decode_png": round(t_read / n, 4),
+                          "points_per_view": pts // n, "s_per_view_batch_by_group": batch_s,
+                          "s_per_view_parts": {"read_decode_png_pinned": round(t_read / n, 4),
                                                "h2d_kernels_d2h": round(t_rec / n, 4),
                                                "ply_write": round(t_ply / n, 4)},
-                          "host_cpus": os.cpu_count()}), flush=True)
+                          "decode_threads": PR.FR.decode_threads(), "host_cpus": os.cpu_count()}), flush=True)
 
 
 if __name__ == "__main__":
