@@ -110,8 +110,10 @@ typedef struct slg_calib {
   int32_t n_row_planes;
   int32_t reserved3;
   /* Optional (NULL: the kernels compute numer per point; same values either way): */
-  const double *col_planes_num; /* device (n_col_planes, 4): col_planes with column 3 replaced by
-                                 * numer = ((n0*Oc0 + n1*Oc1) + n2*Oc2) + d (processing.py:163-165) */
+  const double *col_planes_num; /* device (2, n_col_planes, 2) "pair planes": [0][c] = (n0, n1),
+                                 * [1][c] = (n2, numer), numer = ((n0*Oc0 + n1*Oc1) + n2*Oc2) + d
+                                 * (processing.py:163-166), so a wave's neighbouring column codes
+                                 * gather neighbouring 16-byte pairs */
   const double *row_planes_num; /* the same for the row planes (read by row_mode 2 only) */
 } slg_calib;
 

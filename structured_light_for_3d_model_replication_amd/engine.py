@@ -141,10 +141,11 @@ class DeviceCalib:
         # (processing.py:166,219), evaluated once per plane instead of per point
         oc = np.zeros((3, 1)) if self.oc.size < 3 else self.oc[:3].reshape(3, 1)
 
-        def with_num(tab):
+        def with_num(tab):                          # pair planes [2][P][2] (include/slgpu.h)
             t = _plane_table(tab).copy()
             t[:, 3] = np.dot(t[:, 0:3], oc).flatten() + t[:, 3]
-            return torch.from_numpy(np.ascontiguousarray(t)).to(device)
+            pairs = np.stack([t[:, 0:2], t[:, 2:4]])
+            return torch.from_numpy(np.ascontiguousarray(pairs)).to(device)
 
         self.col_planes_num = with_num(calib["wPlaneCol"])
         self.row_planes_num = (with_num(calib["wPlaneRow"])
