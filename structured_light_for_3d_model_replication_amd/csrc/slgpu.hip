@@ -776,28 +776,49 @@ struct TriOut {
   uint32_t keep;       // bit 0 column stream, bit 1 row stream
 };
 
-// Ray-plane intersection of one valid pixel (processing.py:143-234), fp64 in NumPy's order.
-// FAST (p.rays_fast, checked on the host for every column and row of the image): the
-// Markstein conditions hold for every pixel, so the code is one straight-line block with no
-// per-lane fallback branches -- the same values, and two items per lane interleave (phase B).
-template <int ROW_MODE, int RAYS, bool FAST = false>
-__device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int v) {
-  // Plane rows: (n0, n1, n2, d) row-major, or -- with the precomputed-numerator tables -- split
-  // in pair planes [0][c] = (n0, n1), [1][c] = (n2, numer): a wave's consecutive column codes
-  // then read consecutive 16-byte pairs (8 per cache line) instead of every other 16 bytes of
-  // 32-byte rows, halving the cache lines its two gathers touch.
-  double2 pc01, pc23;
-  if (p.num_pre) {
+// Ray-plane intersection of one valid pixel (processing.py:143-234), fp64 in NumPy's order, in
+// three parts so phase B can issue an item's plane gathers, compute its ray while they are in
+// flight, and only then combine (tri_item chains them for the other callers).
+// NOG (profiling ablations, SLG_DBG bits 10-13): 1 column planes from registers, 2 row planes
+// from registers, 4 column gathers from one broadcast address, 8 row gathers likewise.
+struct TriPlanes {
+  double2 pc01, pc23;  // column plane: (n0, n1), (n2, d or numer)
+  double2 pr01, pr23;  // row plane (row_mode 1/2)
+};
+
+// Plane rows: (n0, n1, n2, d) row-major, or -- with the precomputed-numerator tables -- split
+// in pair planes [0][c] = (n0, n1), [1][c] = (n2, numer): a wave's consecutive column codes
+// then read consecutive 16-byte pairs (8 per cache line) instead of every other 16 bytes of
+// 32-byte rows.
+template <int NOG = 0>
+__device__ inline void tri_planes_col(const MainParams& p, uint32_t code, double2& pc01, double2& pc23) {
+  if constexpr ((NOG & 1) != 0) {
+    pc01 = make_double2(double(code & 0xffffu) * p.rfx, p.rfy);
+    pc23 = make_double2(p.rfx, double(code >> 16) * p.rfy);
+  } else if (p.num_pre) {
     const double2* qc = reinterpret_cast<const double2*>(p.pcol);
-    pc01 = qc[code & 0xffffu];
-    pc23 = qc[p.n_pcol + (code & 0xffffu)];
+    const uint32_t cc = (NOG & 4) ? (code & 1u) : (code & 0xffffu);
+    pc01 = qc[cc];
+    pc23 = qc[p.n_pcol + cc];
   } else {
     const double2* qc = reinterpret_cast<const double2*>(p.pcol + 4 * int64_t(code & 0xffffu));
     pc01 = qc[0];
     pc23 = qc[1];
   }
-  double2 pr01 = make_double2(0, 0), pr23 = make_double2(0, 0);
-  if constexpr (ROW_MODE == 2) {
+}
+
+template <int ROW_MODE, int NOG = 0>
+__device__ inline void tri_planes_row(const MainParams& p, uint32_t code, double2& pr01, double2& pr23) {
+  pr01 = make_double2(0, 0);
+  pr23 = make_double2(0, 0);
+  if constexpr ((NOG & 2) != 0) {
+    pr01 = make_double2(double(code >> 16) * p.rfy, p.rfx);
+    pr23 = make_double2(p.rfy, -2.0);
+  } else if constexpr ((NOG & 8) != 0 && ROW_MODE == 1) {
+    const double2* qr = reinterpret_cast<const double2*>(p.prow + 4 * int64_t(code >> 31));
+    pr01 = qr[0];
+    pr23 = qr[1];
+  } else if constexpr (ROW_MODE == 2) {
     if (p.num_pre) {
       const double2* qr = reinterpret_cast<const double2*>(p.prow);
       pr01 = qr[code >> 16];
@@ -812,7 +833,22 @@ __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int
     pr01 = qr[0];
     pr23 = qr[1];
   }
-  double r0, r1, r2;
+}
+
+template <int ROW_MODE, int NOG = 0>
+__device__ inline TriPlanes tri_planes(const MainParams& p, uint32_t code) {
+  TriPlanes t;
+  tri_planes_col<NOG>(p, code, t.pc01, t.pc23);
+  tri_planes_row<ROW_MODE, NOG>(p, code, t.pr01, t.pr23);
+  return t;
+}
+
+
+// The pixel's unit ray (processing.py:143-156).  FAST (p.rays_fast, checked on the host for
+// every column and row of the image): the Markstein conditions hold for every pixel, so the
+// code is one straight-line block with no per-lane fallback branches -- the same values.
+template <int RAYS, bool FAST = false>
+__device__ inline void tri_ray(const MainParams& p, int u, int v, double& r0, double& r1, double& r2) {
   if (RAYS == SLG_RAYS_PINHOLE) {
     // The same IEEE quotients as the reference, with the divisions by fx, fy (per camera)
     // and by the norm (three per pixel) done as Markstein corrections of one reciprocal.
@@ -838,6 +874,11 @@ __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int
     const int64_t px = int64_t(v) * p.width + u;
     r0 = p.rays[px]; r1 = p.rays[p.n_px + px]; r2 = p.rays[2 * p.n_px + px];
   }
+}
+
+template <int ROW_MODE, bool FAST = false>
+__device__ inline TriOut tri_combine(const MainParams& p, const TriPlanes& pl, double r0, double r1, double r2) {
+  const double2 pc01 = pl.pc01, pc23 = pl.pc23, pr01 = pl.pr01, pr23 = pl.pr23;
   TriOut o;
   const double den = (pc01.x * r0 + pc01.y * r1) + pc23.x * r2;          // np.sum(N*rays, 0)
   // numer = n.Oc + d (processing.py:163-165): precomputed per plane by the caller (column 3 of
@@ -873,6 +914,14 @@ __device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int
     o.keep |= uint32_t(okr) << 1;
   }
   return o;
+}
+
+template <int ROW_MODE, int RAYS, bool FAST = false>
+__device__ inline TriOut tri_item(const MainParams& p, uint32_t code, int u, int v) {
+  const TriPlanes pl = tri_planes<ROW_MODE>(p, code);
+  double r0, r1, r2;
+  tri_ray<RAYS, FAST>(p, u, v, r0, r1, r2);
+  return tri_combine<ROW_MODE, FAST>(p, pl, r0, r1, r2);
 }
 
 // One pixel decoded exactly as decode_lane decodes it, with byte loads and few registers
@@ -1210,20 +1259,30 @@ __device__ inline int2 block_scan(int x, int* s_wtot) {
 // Phase B of main3 for rounds [i, i + G) (item m = tid + 256 * round), FAST path: the G items'
 // loads and fp64 chains are independent, so their plane gathers are in flight together.
 // tri_rounds: i is a compile-time multiple of G (the unrolled group loop); tri_rounds_at: any i.
-template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt>
+template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NOG = 0>
 __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, const uint32_t* s_code,
                                      const uint32_t* s_uv, XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
   const int tid = threadIdx.x;
   TriOut o[G];
+  TriPlanes pl[G];
+  double ra[G][3];
   bool in[G];
+  uint32_t uvs[G];
 #pragma unroll
-  for (int h = 0; h < G; ++h) {
+  for (int h = 0; h < G; ++h) {                    // the G items' plane gathers, all in flight ...
     const int m = tid + kTileBlock * (i + h);
     in[h] = m < n_items;
     const uint32_t sc = s_code[m], suv = s_uv[m];   // m < kTilePx; garbage past n_items masked
-    const uint32_t code = in[h] ? sc : 0u, uv = in[h] ? suv : 0u;
-    o[h] = tri_item<ROW_MODE, RAYS, true>(p, code, int(uv & 0xffffu), int(uv >> 16));
+    const uint32_t code = in[h] ? sc : 0u;
+    uvs[h] = in[h] ? suv : 0u;
+    pl[h] = tri_planes<ROW_MODE, NOG>(p, code);
   }
+#pragma unroll
+  for (int h = 0; h < G; ++h)                      // ... while the rays are computed
+    tri_ray<RAYS, true>(p, int(uvs[h] & 0xffffu), int(uvs[h] >> 16), ra[h][0], ra[h][1], ra[h][2]);
+  __builtin_amdgcn_sched_barrier(0);               // keep the combine (first use of the planes) after them
+#pragma unroll
+  for (int h = 0; h < G; ++h) o[h] = tri_combine<ROW_MODE, true>(p, pl[h], ra[h][0], ra[h][1], ra[h][2]);
 #pragma unroll
   for (int h = 0; h < G; ++h) {
     const uint32_t keep = in[h] ? o[h].keep : 0u;
@@ -1241,10 +1300,10 @@ __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, co
   }
 }
 
-template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt>
+template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NOG = 0>
 __device__ inline void tri_rounds(const MainParams& p, int i, int n_items, const uint32_t* s_code,
                                   const uint32_t* s_uv, XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
-  tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt>(p, i, n_items, s_code, s_uv, pts, km);
+  tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt, NOG>(p, i, n_items, s_code, s_uv, pts, km);
 }
 
 // PROF: the profiling instance (SLG_DBG set): honours the ablation bits of MainParams::dbg and
@@ -1356,20 +1415,31 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     // then a single round, so no empty round is computed.
     const int rounds = (n_items + kB - 1) / kB;
     int i = 0;
+    auto all_rounds = [&](auto nog) {
+      constexpr int NOG = decltype(nog)::value;
 #pragma unroll
-    for (int g = 0; g + SLG_TRI_GROUP <= kIt; g += SLG_TRI_GROUP)
-      if (i + SLG_TRI_GROUP <= rounds) {
-        tri_rounds<SLG_TRI_GROUP, ROW_MODE, RAYS, XT, NS, kIt>(p, g, n_items, s_code, s_uv, pts, km);
-        i = g + SLG_TRI_GROUP;
+      for (int g = 0; g + SLG_TRI_GROUP <= kIt; g += SLG_TRI_GROUP)
+        if (i + SLG_TRI_GROUP <= rounds) {
+          tri_rounds<SLG_TRI_GROUP, ROW_MODE, RAYS, XT, NS, kIt, NOG>(p, g, n_items, s_code, s_uv, pts, km);
+          i = g + SLG_TRI_GROUP;
+        }
+      if (SLG_TRI_GROUP > 2 && i + 2 <= rounds) {
+        tri_rounds_at<2, ROW_MODE, RAYS, XT, NS, kIt, NOG>(p, i, n_items, s_code, s_uv, pts, km);
+        i += 2;
       }
-    if (SLG_TRI_GROUP > 2 && i + 2 <= rounds) {
-      tri_rounds_at<2, ROW_MODE, RAYS, XT, NS, kIt>(p, i, n_items, s_code, s_uv, pts, km);
-      i += 2;
-    }
-    if (i < rounds) {
-      tri_rounds_at<1, ROW_MODE, RAYS, XT, NS, kIt>(p, i, n_items, s_code, s_uv, pts, km);
-      i += 1;
-    }
+      if (i < rounds) {
+        tri_rounds_at<1, ROW_MODE, RAYS, XT, NS, kIt, NOG>(p, i, n_items, s_code, s_uv, pts, km);
+        i += 1;
+      }
+    };
+    const int nog = PROF ? (p.dbg >> 10) & 15 : 0;   // profiling ablations of the plane gathers
+    if (PROF && nog == 3) all_rounds(std::integral_constant<int, PROF ? 3 : 0>());
+    else if (PROF && nog == 1) all_rounds(std::integral_constant<int, PROF ? 1 : 0>());
+    else if (PROF && nog == 2) all_rounds(std::integral_constant<int, PROF ? 2 : 0>());
+    else if (PROF && nog == 4) all_rounds(std::integral_constant<int, PROF ? 4 : 0>());
+    else if (PROF && nog == 8) all_rounds(std::integral_constant<int, PROF ? 8 : 0>());
+    else if (PROF && nog == 12) all_rounds(std::integral_constant<int, PROF ? 12 : 0>());
+    else all_rounds(std::integral_constant<int, 0>());
 #pragma unroll
     for (int r = 0; r < kIt; ++r)
       if (r >= i) {
@@ -1475,10 +1545,20 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       if ((km[s][i] >> lane) & 1ull) {
         const int64_t q = base + before + __popcll(km[s][i] & lt);
         const uint32_t c = s_bgr[tid + kB * i];
-        if (!(PROF && (p.dbg & 128))) {              // PROF ablation bit 7: no XYZ stores
+        bool packed = false;
+        if constexpr (PROF && sizeof(XT) == 4) {     // PROF bit 8: one 16-byte {x, y, z, bgr} record
+          if (p.dbg & 256) {
+            if (q < p.n_px * 3 / 4)
+              reinterpret_cast<uint4*>(gx)[q] = make_uint4(__float_as_uint(float(pts[s][i][0])),
+                  __float_as_uint(float(pts[s][i][1])), __float_as_uint(float(pts[s][i][2])), c);
+            packed = true;
+          }
+        }
+        if (packed) {
+        } else if (!(PROF && (p.dbg & 128))) {       // PROF ablation bit 7: no XYZ stores
           gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
         }
-        if (!(PROF && (p.dbg & 8))) {                // PROF ablation bit 3: no BGR stores
+        if (!packed && !(PROF && (p.dbg & 8))) {     // PROF ablation bit 3: no BGR stores
           gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
         }
       }
@@ -1778,7 +1858,7 @@ int debug_flags() {   // profiling ablations only; unset in production
   return e ? atoi(e) : 0;
 }
 
-constexpr int kMainDbgBits = 1 | 2 | 4 | 8 | 64 | 128;   // bits main3's profiling instance reads
+constexpr int kMainDbgBits = 1 | 2 | 4 | 8 | 64 | 128 | 256 | 512 | 0x3c00;   // 512: the instance alone   // bits main3's profiling instance reads
 
 uint32_t help_after() {   // look-back helper delay; SLG_HELP_AFTER=0 forces the helper (tests)
   const char* e = getenv("SLG_HELP_AFTER");

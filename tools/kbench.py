@@ -96,7 +96,8 @@ def main():
         os.environ.pop("SLG_DBG")
         tags = [("", None)]
         if nb == len(dfr):
-            tags += [(f"_dbg{d}", str(d)) for d in (1, 2, 4, 3, 5, 6, 7, 8, 128, 11, 131)]
+            dl = os.environ.get("KBENCH_DBG", "1,2,4,3,5,6,7,8,128,11,131")
+            tags += [(f"_dbg{d}", str(d)) for d in (int(x) for x in dl.split(",") if x)]
         for tag, dbg in tags:
             if dbg:
                 os.environ["SLG_DBG"] = dbg
@@ -128,7 +129,8 @@ def main():
         n_tiles = (n_px + 2047) // 2048
         parts_off = 65536 + al(2 * n_tiles * 8) + al(n_px * 24) + al(n_px * 3)
         n_wg = n_tiles * nb
-        for extra in (0, 1, 2):                      # + ablations: no wait / trivial tri
+        extras = [int(x) for x in os.environ.get("KBENCH_PHASE_EXTRA", "0,1,2").split(",") if x]
+        for extra in extras:                         # + ablations: no wait / trivial tri / ...
             os.environ["SLG_DBG"] = str(64 | extra)
             recs, us = [], 0.0
             for _ in range(4):

@@ -32,14 +32,18 @@ __device__ inline void acc4(uint32_t (&a)[4], uint32_t p, uint32_t i, int j) {
 
 template <int W>  // load width in dwords: 2 (8 B) or 4 (16 B)
 struct Vec;
-template <> struct Vec<2> { using T = uint2; };
-template <> struct Vec<4> { using T = uint4; };
+typedef unsigned int u32x2e __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
+template <> struct Vec<2> { using T = uint2; using E = u32x2e; };
+template <> struct Vec<4> { using T = uint4; using E = u32x4e; };
 
 __device__ inline uint32_t getw(const uint2& v, int k) { return k == 0 ? v.x : v.y; }
 __device__ inline uint32_t getw(const uint4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
 // One lane decodes PX = 4*W pixels; loads of BATCH (col,row) pair groups are issued together.
-template <int W, int BATCH, int BLOCK>
+// LAYOUT 0: frame-major [view][frame][stride] (the product layout); 1: tile-interleaved
+// [view][tile][frame][TILE] (one contiguous 44*TILE run per workgroup).  NT: non-temporal loads.
+template <int W, int BATCH, int BLOCK, int LAYOUT = 0, int NT = 0>
 __global__ __launch_bounds__(BLOCK) void probe(const uint8_t* frames, int64_t view_bytes, int tiles_per_view,
                                                uint32_t* sink) {
   using V = typename Vec<W>::T;
@@ -49,7 +53,18 @@ __global__ __launch_bounds__(BLOCK) void probe(const uint8_t* frames, int64_t vi
   const uint8_t* f = frames + view * view_bytes;
   int64_t px0 = int64_t(tile) * TILE + int64_t(threadIdx.x) * PX;
   if (px0 >= kNpx) px0 = 0;
-  auto ld = [&](int fr) { return *reinterpret_cast<const V*>(f + fr * kStride + px0); };
+  const int64_t tb = int64_t(tile) * kF * TILE + int64_t(threadIdx.x) * PX;
+  auto ld = [&](int fr) {
+    const uint8_t* a = LAYOUT ? f + tb + fr * TILE : f + fr * kStride + px0;
+    if constexpr (NT) {
+      const typename Vec<W>::E e = __builtin_nontemporal_load(reinterpret_cast<const typename Vec<W>::E*>(a));
+      V v;
+      __builtin_memcpy(&v, &e, sizeof(v));
+      return v;
+    } else {
+      return *reinterpret_cast<const V*>(a);
+    }
+  };
   const V w = ld(0), b = ld(1);
   uint32_t ac[2 * W] = {}, ar[2 * W] = {};
 #pragma unroll
@@ -100,11 +115,11 @@ __global__ void fill(uint8_t* p, int64_t n, uint32_t seed) {
   }
 }
 
-template <int W, int BATCH, int BLOCK>
+template <int W, int BATCH, int BLOCK, int LAYOUT = 0, int NT = 0>
 void run(const char* name, const uint8_t* frames, int n_views, int views_per_launch, uint32_t* sink) {
   constexpr int TILE = BLOCK * 4 * W;
   const int tpv = int((kNpx + TILE - 1) / TILE);
-  const int64_t vb = int64_t(kF) * kStride;
+  const int64_t vb = int64_t(kF) * kStride + 64 * 4096;  // room for the interleaved tail tile
   hipEvent_t a, b;
   CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   std::vector<float> ts;
@@ -112,7 +127,7 @@ void run(const char* name, const uint8_t* frames, int n_views, int views_per_lau
     const int v0 = (it * views_per_launch) % n_views;
     const int nv = std::min(views_per_launch, n_views - v0);
     CK(hipEventRecord(a, 0));
-    hipLaunchKernelGGL((probe<W, BATCH, BLOCK>), dim3(tpv * nv), dim3(BLOCK), 0, 0, frames + v0 * vb, vb, tpv, sink);
+    hipLaunchKernelGGL((probe<W, BATCH, BLOCK, LAYOUT, NT>), dim3(tpv * nv), dim3(BLOCK), 0, 0, frames + v0 * vb, vb, tpv, sink);
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
     float ms; CK(hipEventElapsedTime(&ms, a, b));
@@ -125,22 +140,22 @@ void run(const char* name, const uint8_t* frames, int n_views, int views_per_lau
 
 int main() {
   const int n_views = 12;
-  const int64_t vb = int64_t(kF) * kStride;
+  const int64_t vb = int64_t(kF) * kStride + 64 * 4096;
   uint8_t* frames; uint32_t* sink;
   CK(hipMalloc(&frames, vb * n_views));
   CK(hipMalloc(&sink, 4096 * 4));
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, frames, vb * n_views, 7u);
   CK(hipDeviceSynchronize());
-  for (int vpl : {1, 6}) {
-    run<2, 8, 256>("u2 8px batch8 blk256", frames, n_views, vpl, sink);
-    run<2, 11, 256>("u2 8px batch11 blk256", frames, n_views, vpl, sink);
-    run<2, 4, 256>("u2 8px batch4 blk256", frames, n_views, vpl, sink);
-    run<4, 4, 256>("u4 16px batch4 blk256", frames, n_views, vpl, sink);
-    run<4, 6, 256>("u4 16px batch6 blk256", frames, n_views, vpl, sink);
-    run<4, 11, 256>("u4 16px batch11 blk256", frames, n_views, vpl, sink);
-    run<4, 4, 128>("u4 16px batch4 blk128", frames, n_views, vpl, sink);
-    run<4, 6, 64>("u4 16px batch6 blk64", frames, n_views, vpl, sink);
-    run<2, 11, 64>("u2 8px batch11 blk64", frames, n_views, vpl, sink);
+  for (int vpl : {12}) {
+    run<2, 11, 256, 0, 0>("u2 8px batch11 frame-major", frames, n_views, vpl, sink);
+    run<2, 11, 256, 0, 1>("u2 8px batch11 frame-major nt", frames, n_views, vpl, sink);
+    run<2, 11, 256, 1, 0>("u2 8px batch11 tile-interleaved", frames, n_views, vpl, sink);
+    run<2, 11, 256, 1, 1>("u2 8px batch11 tile-interleaved nt", frames, n_views, vpl, sink);
+    run<4, 11, 256, 0, 1>("u4 16px batch11 frame-major nt", frames, n_views, vpl, sink);
+    run<4, 11, 256, 1, 1>("u4 16px batch11 tile-interleaved nt", frames, n_views, vpl, sink);
+    run<4, 6, 256, 0, 1>("u4 16px batch6 frame-major nt", frames, n_views, vpl, sink);
+    run<4, 6, 256, 1, 1>("u4 16px batch6 tile-interleaved nt", frames, n_views, vpl, sink);
+    run<2, 11, 256, 0, 1>("u2 8px batch11 frame-major nt (again)", frames, n_views, vpl, sink);
   }
   return 0;
 }
