@@ -8,12 +8,13 @@
 //   stats_kernel      white/black histograms (+ max contrast) -> last-arriving workgroup turns
 //                     them into integer mask thresholds (Otsu as OpenCV, or NumPy percentile);
 //                     also zeroes the compaction state of the next main launch.
-//   main3_kernel<...> fused decode + triangulate + ordered compaction, one 2048-pixel tile per
-//                     workgroup (256 lanes x 8 pixels), up to 16 views per launch: streams the
+//   main3_kernel<...> fused decode + triangulate + ordered compaction, one 4096-pixel tile per
+//                     workgroup (512 lanes x 8 pixels), up to 16 views per launch: streams the
 //                     used frames with 8-byte-per-lane coalesced loads, SWAR byte compares,
 //                     packed 16-bit Gray->binary, wave-private LDS compaction of valid pixels,
-//                     fp64 ray-plane intersection, decoupled look-back over in-order claimed
-//                     tiles, compacted stores straight from registers.
+//                     fp64 ray-plane intersection, decoupled look-back over static tile ids,
+//                     compacted stores straight from registers; the grid's first workgroups
+//                     can turn a carried batch's Otsu partials into thresholds.
 //   decode_maps_kernel  the decode alone, to correspondence maps (slg_decode).
 //   row_tail_kernel   row_mode 2: moves the row cloud behind the column cloud.
 //   pinhole_kernel    bitwise Nc == pinhole(cam_K) test.
@@ -46,10 +47,11 @@ namespace {
 constexpr int kBlock = 256;                 // 4 waves of 64
 constexpr int kPx = 8;                      // pixels per lane (one 8-byte load per frame)
 #ifndef SLG_TILE_BLOCK
-#define SLG_TILE_BLOCK 256
+#define SLG_TILE_BLOCK 512
 #endif
-constexpr int kTileBlock = SLG_TILE_BLOCK;  // main3 workgroup (512 measured slower: 31.3 vs 30.2 us/view)
-constexpr int kTilePx = kTileBlock * kPx;   // 2048 pixels per main3 tile (one look-back entry)
+constexpr int kTileBlock = SLG_TILE_BLOCK;  // main3 workgroup: 512 lanes, 322.6 vs 331.3 us per
+                                            // 12-view launch with 256 (half the look-backs per pixel)
+constexpr int kTilePx = kTileBlock * kPx;   // 4096 pixels per main3 tile (one look-back entry)
 constexpr int kMapsPx = kBlock * kPx;       // 2048 pixels per decode_maps workgroup
 constexpr int kMaxBits = 15;                // packed 16-bit code lanes
 #ifndef SLG_LOOK_K
@@ -544,27 +546,30 @@ __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint
                                 int64_t n_state_words, int64_t pad_zero, int block, int n_blocks,
                                 uint32_t* hg, uint32_t* s_last) {
   const int tid = threadIdx.x, wave = tid >> 6;
+  const bool act = tid < kBlock;               // the work is laid out for 256 lanes (a 512-lane
   uint32_t* hist_part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + kHistPartOff);
   uint64_t* states = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + states_off(n_px));
-  for (int64_t i = int64_t(block) * kBlock + tid; i < n_state_words; i += int64_t(n_blocks) * kBlock)
-    states[i] = 0;
-  if (block == 0 && tid == 0) ws->tile_counter = 0;
+  if (act) {                                   // main3 workgroup's upper half only syncs)
+    for (int64_t i = int64_t(block) * kBlock + tid; i < n_state_words; i += int64_t(n_blocks) * kBlock)
+      states[i] = 0;
+    if (block == 0 && tid == 0) ws->tile_counter = 0;
 
-  // thread t owns packed word t (bins 2t, 2t+1 of [white 0..255 | clip 256..511])
-  const int64_t per = (n_parts + n_blocks - 1) / n_blocks;
-  const int64_t t0 = int64_t(block) * per, t1 = t0 + per < n_parts ? t0 + per : n_parts;
-  uint32_t a0 = 0, a1 = 0;
-  for (int64_t k0 = t0; k0 < t1; k0 += kPartsInFlight) {
-    uint32_t v[kPartsInFlight];
+    // thread t owns packed word t (bins 2t, 2t+1 of [white 0..255 | clip 256..511])
+    const int64_t per = (n_parts + n_blocks - 1) / n_blocks;
+    const int64_t t0 = int64_t(block) * per, t1 = t0 + per < n_parts ? t0 + per : n_parts;
+    uint32_t a0 = 0, a1 = 0;
+    for (int64_t k0 = t0; k0 < t1; k0 += kPartsInFlight) {
+      uint32_t v[kPartsInFlight];
 #pragma unroll
-    for (int j = 0; j < kPartsInFlight; ++j)
-      v[j] = k0 + j < t1 ? pp[(k0 + j) * kPartWords + tid] : 0u;
+      for (int j = 0; j < kPartsInFlight; ++j)
+        v[j] = k0 + j < t1 ? pp[(k0 + j) * kPartWords + tid] : 0u;
 #pragma unroll
-    for (int j = 0; j < kPartsInFlight; ++j) { a0 += v[j] & 0xffffu; a1 += v[j] >> 16; }
+      for (int j = 0; j < kPartsInFlight; ++j) { a0 += v[j] & 0xffffu; a1 += v[j] >> 16; }
+    }
+    uint32_t* dst = hist_part + (block % kHistCopies) * 512 + 2 * tid;
+    if (a0) atomicAdd(dst, a0);
+    if (a1) atomicAdd(dst + 1, a1);
   }
-  uint32_t* dst = hist_part + (block % kHistCopies) * 512 + 2 * tid;
-  if (a0) atomicAdd(dst, a0);
-  if (a1) atomicAdd(dst + 1, a1);
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -581,7 +586,7 @@ __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  for (int i = tid; i < 512; i += kBlock) {
+  for (int i = tid; act && i < 512; i += kBlock) {
     uint32_t acc = 0;
 #pragma unroll
     for (int c = 0; c < kHistCopies; ++c)
@@ -597,7 +602,7 @@ __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint
       if (wave == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
     }
   }
-  for (int i = tid; i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
+  for (int i = tid; act && i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
   if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
 }
 
@@ -1082,8 +1087,8 @@ __global__ __launch_bounds__(kBlock) void decode_maps_kernel(MainParams p) {
 }
 
 // ------------------------------------------------------------------ main3: occupancy-first fused kernel
-// One launch covers up to kMaxViews views of one geometry (grid = views x tiles, view-major).
-// Per 256-lane workgroup and 2048-pixel tile:
+// One launch covers up to kMaxViews views of one geometry (grid = tiles x views, views
+// interleaved).  Per kTileBlock-lane workgroup and kTilePx-pixel tile:
 //  A  every lane decodes its 8 pixels (all used frames in flight, 8-byte coalesced loads); a
 //     block scan compacts the tile's valid pixels into LDS items (code, BGR, pixel offset);
 //  B  the lanes triangulate the items one workgroup-width at a time (fp64, NumPy order) --
@@ -1093,8 +1098,8 @@ __global__ __launch_bounds__(kBlock) void decode_maps_kernel(MainParams p) {
 //     decoupled look-back (helping a long-silent predecessor, so waiting always ends);
 //  D  each lane stores its points at offset + rank: consecutive lanes write consecutive
 //     points, so the compacted stores coalesce without an LDS staging copy.
-// 20 KB of LDS and no point staging keep several workgroups per CU resident, so one tile's
-// decode stream overlaps other tiles' fp64 work and look-back.
+// 49 KB of LDS (24 KB at 256 lanes) and no point staging keep two 512-lane workgroups per CU
+// resident, so one tile's decode stream overlaps another's fp64 work and look-back.
 constexpr int kMaxViews = 16;
 #ifndef SLG_DECODE_BATCH
 #define SLG_DECODE_BATCH 11                // pairs per axis in flight per lane (4/6/8/11: 31.7/30.3/28.7/27.5 us/view)

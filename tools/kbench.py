@@ -126,7 +126,8 @@ def main():
         bclouds = [E.Cloud(H * W, 1, False) for _ in range(nb)]
         pb = beng.prepare(dfr, cfg, dcal, bclouds, 1)
         al = lambda x: (x + 255) // 256 * 256
-        n_tiles = (n_px + 2047) // 2048
+        tpx = int(os.environ.get("SLG_TILE_PX", "4096"))     # main3 tile (kTilePx)
+        n_tiles = (n_px + tpx - 1) // tpx
         parts_off = 65536 + al(2 * n_tiles * 8) + al(n_px * 24) + al(n_px * 3)
         n_wg = n_tiles * nb
         extras = [int(x) for x in os.environ.get("KBENCH_PHASE_EXTRA", "0,1,2").split(",") if x]

@@ -43,9 +43,9 @@ __device__ inline uint32_t getw(const uint4& v, int k) { return k == 0 ? v.x : k
 // One lane decodes PX = 4*W pixels; loads of BATCH (col,row) pair groups are issued together.
 // LAYOUT 0: frame-major [view][frame][stride] (the product layout); 1: tile-interleaved
 // [view][tile][frame][TILE] (one contiguous 44*TILE run per workgroup).  NT: non-temporal loads.
-template <int W, int BATCH, int BLOCK, int LAYOUT = 0, int NT = 0>
+template <int W, int BATCH, int BLOCK, int LAYOUT = 0, int NT = 0, int STORE = 0>
 __global__ __launch_bounds__(BLOCK) void probe(const uint8_t* frames, int64_t view_bytes, int tiles_per_view,
-                                               uint32_t* sink) {
+                                               uint32_t* sink, float* xyz, uint8_t* bgr) {
   using V = typename Vec<W>::T;
   constexpr int PX = 4 * W;
   constexpr int TILE = BLOCK * PX;
@@ -103,6 +103,21 @@ __global__ __launch_bounds__(BLOCK) void probe(const uint8_t* frames, int64_t vi
     const uint32_t wv = getw(w, k), bv = getw(b, k);
     h ^= __builtin_amdgcn_perm(wv, bv, 0x05010400u) + (wv > 0x40404040u);
   }
+  if constexpr (STORE) {
+    // the cloud of this tile: 57 % of its pixels (the C2 bench's valid fraction), compacted
+    // points at consecutive addresses, one point per lane per round (as main3 phase D)
+    constexpr int TILE = BLOCK * 4 * W;
+    const int64_t base = int64_t(blockIdx.x) * (TILE * 57 / 100);
+    for (int i = threadIdx.x; i < TILE * 57 / 100; i += BLOCK) {
+      const int64_t q = base + i;
+      if constexpr (STORE == 1) {
+        xyz[3 * q] = float(h); xyz[3 * q + 1] = float(h + 1); xyz[3 * q + 2] = float(h + 2);
+        bgr[3 * q] = uint8_t(h); bgr[3 * q + 1] = uint8_t(h >> 8); bgr[3 * q + 2] = uint8_t(h >> 16);
+      } else {
+        reinterpret_cast<uint4*>(xyz)[q] = make_uint4(h, h + 1, h + 2, h + 3);
+      }
+    }
+  }
   for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
   if ((threadIdx.x & 63) == 0) atomicAdd(sink + (blockIdx.x & 1023), h);
 }
@@ -115,8 +130,9 @@ __global__ void fill(uint8_t* p, int64_t n, uint32_t seed) {
   }
 }
 
-template <int W, int BATCH, int BLOCK, int LAYOUT = 0, int NT = 0>
-void run(const char* name, const uint8_t* frames, int n_views, int views_per_launch, uint32_t* sink) {
+template <int W, int BATCH, int BLOCK, int LAYOUT = 0, int NT = 0, int STORE = 0>
+void run(const char* name, const uint8_t* frames, int n_views, int views_per_launch, uint32_t* sink,
+         float* xyz = nullptr, uint8_t* bgr = nullptr) {
   constexpr int TILE = BLOCK * 4 * W;
   const int tpv = int((kNpx + TILE - 1) / TILE);
   const int64_t vb = int64_t(kF) * kStride + 64 * 4096;  // room for the interleaved tail tile
@@ -127,7 +143,7 @@ void run(const char* name, const uint8_t* frames, int n_views, int views_per_lau
     const int v0 = (it * views_per_launch) % n_views;
     const int nv = std::min(views_per_launch, n_views - v0);
     CK(hipEventRecord(a, 0));
-    hipLaunchKernelGGL((probe<W, BATCH, BLOCK, LAYOUT, NT>), dim3(tpv * nv), dim3(BLOCK), 0, 0, frames + v0 * vb, vb, tpv, sink);
+    hipLaunchKernelGGL((probe<W, BATCH, BLOCK, LAYOUT, NT, STORE>), dim3(tpv * nv), dim3(BLOCK), 0, 0, frames + v0 * vb, vb, tpv, sink, xyz, bgr);
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
     float ms; CK(hipEventElapsedTime(&ms, a, b));
@@ -146,15 +162,15 @@ int main() {
   CK(hipMalloc(&sink, 4096 * 4));
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, frames, vb * n_views, 7u);
   CK(hipDeviceSynchronize());
+  float* xyz; uint8_t* bgr;
+  CK(hipMalloc(&xyz, int64_t(n_views) * kNpx * 16));
+  CK(hipMalloc(&bgr, int64_t(n_views) * kNpx * 3));
   for (int vpl : {12}) {
-    run<2, 11, 256, 0, 0>("u2 8px batch11 frame-major", frames, n_views, vpl, sink);
     run<2, 11, 256, 0, 1>("u2 8px batch11 frame-major nt", frames, n_views, vpl, sink);
-    run<2, 11, 256, 1, 0>("u2 8px batch11 tile-interleaved", frames, n_views, vpl, sink);
-    run<2, 11, 256, 1, 1>("u2 8px batch11 tile-interleaved nt", frames, n_views, vpl, sink);
-    run<4, 11, 256, 0, 1>("u4 16px batch11 frame-major nt", frames, n_views, vpl, sink);
-    run<4, 11, 256, 1, 1>("u4 16px batch11 tile-interleaved nt", frames, n_views, vpl, sink);
-    run<4, 6, 256, 0, 1>("u4 16px batch6 frame-major nt", frames, n_views, vpl, sink);
-    run<4, 6, 256, 1, 1>("u4 16px batch6 tile-interleaved nt", frames, n_views, vpl, sink);
+    run<2, 11, 256, 0, 1, 1>("  + cloud stores (12 B + 3 B)", frames, n_views, vpl, sink, xyz, bgr);
+    run<2, 11, 256, 0, 1, 2>("  + cloud stores (16-B records)", frames, n_views, vpl, sink, xyz, bgr);
+    run<2, 11, 512, 0, 1>("u2 8px batch11 blk512 nt", frames, n_views, vpl, sink);
+    run<2, 11, 512, 0, 1, 1>("  + cloud stores (12 B + 3 B)", frames, n_views, vpl, sink, xyz, bgr);
     run<2, 11, 256, 0, 1>("u2 8px batch11 frame-major nt (again)", frames, n_views, vpl, sink);
   }
   return 0;
