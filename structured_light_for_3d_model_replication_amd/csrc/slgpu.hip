@@ -795,12 +795,13 @@ struct TriPlanes {
 // in pair planes [0][c] = (n0, n1), [1][c] = (n2, numer): a wave's consecutive column codes
 // then read consecutive 16-byte pairs (8 per cache line) instead of every other 16 bytes of
 // 32-byte rows.
-template <int NOG = 0>
+// NP: 0 reads p.num_pre at run time, 1 / 2 take it as set / clear (phase B picks per workgroup).
+template <int NOG = 0, int NP = 0>
 __device__ inline void tri_planes_col(const MainParams& p, uint32_t code, double2& pc01, double2& pc23) {
   if constexpr ((NOG & 1) != 0) {
     pc01 = make_double2(double(code & 0xffffu) * p.rfx, p.rfy);
     pc23 = make_double2(p.rfx, double(code >> 16) * p.rfy);
-  } else if (p.num_pre) {
+  } else if (NP == 1 || (NP == 0 && p.num_pre)) {
     const double2* qc = reinterpret_cast<const double2*>(p.pcol);
     const uint32_t cc = (NOG & 4) ? (code & 1u) : (code & 0xffffu);
     pc01 = qc[cc];
@@ -812,7 +813,7 @@ __device__ inline void tri_planes_col(const MainParams& p, uint32_t code, double
   }
 }
 
-template <int ROW_MODE, int NOG = 0>
+template <int ROW_MODE, int NOG = 0, int NP = 0>
 __device__ inline void tri_planes_row(const MainParams& p, uint32_t code, double2& pr01, double2& pr23) {
   pr01 = make_double2(0, 0);
   pr23 = make_double2(0, 0);
@@ -824,7 +825,7 @@ __device__ inline void tri_planes_row(const MainParams& p, uint32_t code, double
     pr01 = qr[0];
     pr23 = qr[1];
   } else if constexpr (ROW_MODE == 2) {
-    if (p.num_pre) {
+    if (NP == 1 || (NP == 0 && p.num_pre)) {
       const double2* qr = reinterpret_cast<const double2*>(p.prow);
       pr01 = qr[code >> 16];
       pr23 = qr[p.n_prow + (code >> 16)];
@@ -840,11 +841,11 @@ __device__ inline void tri_planes_row(const MainParams& p, uint32_t code, double
   }
 }
 
-template <int ROW_MODE, int NOG = 0>
+template <int ROW_MODE, int NOG = 0, int NP = 0>
 __device__ inline TriPlanes tri_planes(const MainParams& p, uint32_t code) {
   TriPlanes t;
-  tri_planes_col<NOG>(p, code, t.pc01, t.pc23);
-  tri_planes_row<ROW_MODE, NOG>(p, code, t.pr01, t.pr23);
+  tri_planes_col<NOG, NP>(p, code, t.pc01, t.pc23);
+  tri_planes_row<ROW_MODE, NOG, NP>(p, code, t.pr01, t.pr23);
   return t;
 }
 
@@ -881,14 +882,15 @@ __device__ inline void tri_ray(const MainParams& p, int u, int v, double& r0, do
   }
 }
 
-template <int ROW_MODE, bool FAST = false>
+template <int ROW_MODE, bool FAST = false, int NP = 0>
 __device__ inline TriOut tri_combine(const MainParams& p, const TriPlanes& pl, double r0, double r1, double r2) {
+  const bool num_pre = NP == 1 || (NP == 0 && p.num_pre);
   const double2 pc01 = pl.pc01, pc23 = pl.pc23, pr01 = pl.pr01, pr23 = pl.pr23;
   TriOut o;
   const double den = (pc01.x * r0 + pc01.y * r1) + pc23.x * r2;          // np.sum(N*rays, 0)
   // numer = n.Oc + d (processing.py:163-165): precomputed per plane by the caller (column 3 of
   // the table) or computed here
-  const double num = p.num_pre ? pc23.y : ((pc01.x * p.o0 + pc01.y * p.o1) + pc23.x * p.o2) + pc23.y;
+  const double num = num_pre ? pc23.y : ((pc01.x * p.o0 + pc01.y * p.o1) + pc23.x * p.o2) + pc23.y;
   const bool okc = fabs(den) > 1e-6;
   double t;
   if constexpr (FAST) {
@@ -906,7 +908,7 @@ __device__ inline TriOut tri_combine(const MainParams& p, const TriPlanes& pl, d
   }
   if constexpr (ROW_MODE == 2) {                          // independent row cloud, :218-228
     const double dr = (pr01.x * r0 + pr01.y * r1) + pr23.x * r2;
-    const double nr = p.num_pre ? pr23.y : ((pr01.x * p.o0 + pr01.y * p.o1) + pr23.x * p.o2) + pr23.y;
+    const double nr = num_pre ? pr23.y : ((pr01.x * p.o0 + pr01.y * p.o1) + pr23.x * p.o2) + pr23.y;
     const bool okr = fabs(dr) > 1e-6;
     double tr;
     if constexpr (FAST) {
@@ -1105,7 +1107,7 @@ constexpr int kMaxViews = 16;
 #define SLG_DECODE_BATCH 11                // pairs per axis in flight per lane (4/6/8/11: 31.7/30.3/28.7/27.5 us/view)
 #endif
 #ifndef SLG_TRI_GROUP
-#define SLG_TRI_GROUP 2                    // phase B: rounds (items per lane) computed per step
+#define SLG_TRI_GROUP 4                    // phase B: rounds (items per lane) whose gathers are in flight together
 #endif
 #ifndef SLG_M3_WAVES
 #define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
@@ -1264,7 +1266,7 @@ __device__ inline int2 block_scan(int x, int* s_wtot) {
 // Phase B of main3 for rounds [i, i + G) (item m = tid + 256 * round), FAST path: the G items'
 // loads and fp64 chains are independent, so their plane gathers are in flight together.
 // tri_rounds: i is a compile-time multiple of G (the unrolled group loop); tri_rounds_at: any i.
-template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NOG = 0>
+template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NOG = 0, int NP = 0>
 __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, const uint32_t* s_code,
                                      const uint32_t* s_uv, XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
   const int tid = threadIdx.x;
@@ -1280,14 +1282,14 @@ __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, co
     const uint32_t sc = s_code[m], suv = s_uv[m];   // m < kTilePx; garbage past n_items masked
     const uint32_t code = in[h] ? sc : 0u;
     uvs[h] = in[h] ? suv : 0u;
-    pl[h] = tri_planes<ROW_MODE, NOG>(p, code);
+    pl[h] = tri_planes<ROW_MODE, NOG, NP>(p, code);
   }
 #pragma unroll
   for (int h = 0; h < G; ++h)                      // ... while the rays are computed
     tri_ray<RAYS, true>(p, int(uvs[h] & 0xffffu), int(uvs[h] >> 16), ra[h][0], ra[h][1], ra[h][2]);
   __builtin_amdgcn_sched_barrier(0);               // keep the combine (first use of the planes) after them
 #pragma unroll
-  for (int h = 0; h < G; ++h) o[h] = tri_combine<ROW_MODE, true>(p, pl[h], ra[h][0], ra[h][1], ra[h][2]);
+  for (int h = 0; h < G; ++h) o[h] = tri_combine<ROW_MODE, true, NP>(p, pl[h], ra[h][0], ra[h][1], ra[h][2]);
 #pragma unroll
   for (int h = 0; h < G; ++h) {
     const uint32_t keep = in[h] ? o[h].keep : 0u;
@@ -1305,10 +1307,10 @@ __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, co
   }
 }
 
-template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NOG = 0>
+template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NOG = 0, int NP = 0>
 __device__ inline void tri_rounds(const MainParams& p, int i, int n_items, const uint32_t* s_code,
                                   const uint32_t* s_uv, XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
-  tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt, NOG>(p, i, n_items, s_code, s_uv, pts, km);
+  tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_code, s_uv, pts, km);
 }
 
 // PROF: the profiling instance (SLG_DBG set): honours the ablation bits of MainParams::dbg and
@@ -1420,31 +1422,36 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     // then a single round, so no empty round is computed.
     const int rounds = (n_items + kB - 1) / kB;
     int i = 0;
-    auto all_rounds = [&](auto nog) {
+    auto all_rounds = [&](auto nog, auto np) {
       constexpr int NOG = decltype(nog)::value;
+      constexpr int NP = decltype(np)::value;
 #pragma unroll
       for (int g = 0; g + SLG_TRI_GROUP <= kIt; g += SLG_TRI_GROUP)
         if (i + SLG_TRI_GROUP <= rounds) {
-          tri_rounds<SLG_TRI_GROUP, ROW_MODE, RAYS, XT, NS, kIt, NOG>(p, g, n_items, s_code, s_uv, pts, km);
+          tri_rounds<SLG_TRI_GROUP, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, g, n_items, s_code, s_uv, pts, km);
           i = g + SLG_TRI_GROUP;
         }
       if (SLG_TRI_GROUP > 2 && i + 2 <= rounds) {
-        tri_rounds_at<2, ROW_MODE, RAYS, XT, NS, kIt, NOG>(p, i, n_items, s_code, s_uv, pts, km);
+        tri_rounds_at<2, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_code, s_uv, pts, km);
         i += 2;
       }
       if (i < rounds) {
-        tri_rounds_at<1, ROW_MODE, RAYS, XT, NS, kIt, NOG>(p, i, n_items, s_code, s_uv, pts, km);
+        tri_rounds_at<1, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_code, s_uv, pts, km);
         i += 1;
       }
     };
     const int nog = PROF ? (p.dbg >> 10) & 15 : 0;   // profiling ablations of the plane gathers
-    if (PROF && nog == 3) all_rounds(std::integral_constant<int, PROF ? 3 : 0>());
-    else if (PROF && nog == 1) all_rounds(std::integral_constant<int, PROF ? 1 : 0>());
-    else if (PROF && nog == 2) all_rounds(std::integral_constant<int, PROF ? 2 : 0>());
-    else if (PROF && nog == 4) all_rounds(std::integral_constant<int, PROF ? 4 : 0>());
-    else if (PROF && nog == 8) all_rounds(std::integral_constant<int, PROF ? 8 : 0>());
-    else if (PROF && nog == 12) all_rounds(std::integral_constant<int, PROF ? 12 : 0>());
-    else all_rounds(std::integral_constant<int, 0>());
+    using NP0 = std::integral_constant<int, 0>;
+    if (PROF && nog == 3) all_rounds(std::integral_constant<int, PROF ? 3 : 0>(), NP0());
+    else if (PROF && nog == 1) all_rounds(std::integral_constant<int, PROF ? 1 : 0>(), NP0());
+    else if (PROF && nog == 2) all_rounds(std::integral_constant<int, PROF ? 2 : 0>(), NP0());
+    else if (PROF && nog == 4) all_rounds(std::integral_constant<int, PROF ? 4 : 0>(), NP0());
+    else if (PROF && nog == 8) all_rounds(std::integral_constant<int, PROF ? 8 : 0>(), NP0());
+    else if (PROF && nog == 12) all_rounds(std::integral_constant<int, PROF ? 12 : 0>(), NP0());
+    // numerator tables or not: a block-uniform choice between two straight-line instances,
+    // so neither computes the other's numerator and selects
+    else if (p.num_pre) all_rounds(NP0(), std::integral_constant<int, 1>());
+    else all_rounds(NP0(), std::integral_constant<int, 2>());
 #pragma unroll
     for (int r = 0; r < kIt; ++r)
       if (r >= i) {
