@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Copy a gpu_profile.sh run (gpurun_out/<tag>) into profiles/<tag>/ and summarise it.
 
-  python tools/summarize_profile.py r1b [--kernel main3_kernel] [--tiles-per-view 1013]
+  python tools/summarize_profile.py r1b [--kernel main3_kernel] [--tiles-per-view 507]
 
 Writes profiles/<tag>/{bench.json, kernel_stats.csv, kernel_by_grid.json, pmc_summary.json} and
 refreshes profiles/pmc_main_kernel.json, which bench.py reads for `roofline.traffic`.
@@ -23,7 +23,7 @@ import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LANES = 256
+LANES = 512                      # main3 workgroup (kTileBlock)
 
 
 def rows_of(path, kernel):
@@ -37,7 +37,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
     ap.add_argument("--kernel", default="main3_kernel")
-    ap.add_argument("--tiles-per-view", type=int, default=1013, help="ceil(1920*1080 / 2048)")
+    ap.add_argument("--tiles-per-view", type=int, default=507, help="ceil(1920*1080 / 4096)")
     ap.add_argument("--no-refresh", action="store_true",
                     help="leave profiles/pmc_main_kernel.json (bench.py's C2 traffic) untouched")
     a = ap.parse_args()
@@ -54,9 +54,11 @@ def main():
     by_grid = collections.defaultdict(list)
     for r in rows_of(os.path.join(src, "trace", "trace_kernel_trace.csv"), a.kernel):
         by_grid[int(r["Grid_Size_X"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    trace = {str(g): {"views": g / grid_threads_per_view, "launches": len(d),
+    # a pipelined launch also carries its finishing workgroups (fewer than one view's tiles)
+    vof = lambda g: max(1, g // grid_threads_per_view)
+    trace = {str(g): {"views": vof(g), "launches": len(d),
                       "avg_us": round(statistics.mean(d), 2),
-                      "avg_us_per_view": round(statistics.mean(d) / (g / grid_threads_per_view), 2)}
+                      "avg_us_per_view": round(statistics.mean(d) / vof(g), 2)}
              for g, d in sorted(by_grid.items())}
     with open(os.path.join(dst, "kernel_by_grid.json"), "w") as f:
         json.dump({"kernel": a.kernel, "by_grid_threads": trace}, f, indent=1)
@@ -69,7 +71,7 @@ def main():
         rows = rows_of(os.path.join(src, pmc, f"{pmc}_counter_collection.csv"), a.kernel)
         rows = [r for r in rows if r["Counter_Name"] == key]
         if rows:
-            views = sum(int(r["Grid_Size"]) / grid_threads_per_view for r in rows)
+            views = sum(vof(int(r["Grid_Size"])) for r in rows)
             per[key] = sum(float(r["Counter_Value"]) * scale for r in rows) / views
             out[key.lower() + "_bytes_per_view"] = round(per[key])
             out[key.lower() + "_launches"] = len(rows)
