@@ -1057,6 +1057,72 @@ __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int ag
   return true;
 }
 
+#ifndef SLG_SCALAR_LB
+#define SLG_SCALAR_LB 1                    // look-back polls through the scalar path (lookback_scalar)
+#endif
+
+// Look-back words st[b .. b+7] read by one scalar load that misses the scalar cache (glc): the
+// poll goes to L2 without queueing behind the co-resident workgroup's frame stream in the
+// CU's vector-memory pipeline (a vector poll waits behind up to ~180 KB of streaming loads).
+__device__ inline void ld_state8_scalar(const uint64_t* p, uint64_t (&v)[8]) {
+  typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+  u32x16 r;
+  asm volatile("s_load_dwordx16 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = uint64_t(r[2 * k]) | (uint64_t(r[2 * k + 1]) << 32);
+}
+
+// lookback_try's contract (same returns, same helper hand-off), polled 8 predecessors at a
+// time with wave-uniform scalar loads, newest first: aggregates are summed as they appear and
+// the walk stops at the first inclusive prefix; an unpublished entry is re-polled after a
+// capped back-off.  Published values never change (0 -> aggregate -> inclusive), so a stale
+// read only delays the walk, never changes the sum.
+template <bool PROF>
+__device__ bool lookback_scalar(const MainParams& p, uint64_t* st, int tile, int agg, uint64_t& excl_out,
+                                int& help_tile, uint32_t& polls, uint32_t& naps) {
+  const int lane = threadIdx.x & 63;
+  if (PROF && (p.dbg & 1)) { excl_out = uint64_t(tile) * kTilePx; return true; }   // ablation: no wait
+  if (tile == 0) {
+    if (lane == 0) st_state(&st[0], kFlagInc | uint64_t(agg));
+    excl_out = 0;
+    return true;
+  }
+  if (lane == 0) st_state(&st[tile], kFlagAgg | uint64_t(agg));
+  uint64_t excl = 0;
+  int j = tile - 1;                          // newest predecessor not summed yet
+  unsigned slept = 0, nap = 1;
+  for (;;) {
+    ++polls;
+    const int b = j >= 7 ? j - 7 : 0;
+    uint64_t v[8];
+    ld_state8_scalar(st + b, v);
+    bool done = false, stall = false;
+#pragma unroll
+    for (int k = 7; k >= 0; --k) {
+      if (done || stall || b + k > j) continue;
+      const uint64_t f = v[k] >> 62;
+      if (f == 0) { stall = true; continue; }
+      excl += v[k] & kValMask;
+      j = b + k - 1;
+      done = f == 2;
+    }
+    if (done || j < 0) break;
+    if (stall) {
+      if (slept >= p.help_after) {
+        help_tile = j;
+        return false;
+      }
+      for (unsigned z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(2);
+      slept += nap;
+      naps += nap;
+      nap = nap < kNapCap ? nap * 2 : kNapCap;
+    }
+  }
+  if (lane == 0) st_state(&st[tile], kFlagInc | (excl + uint64_t(agg)));
+  excl_out = excl;
+  return true;
+}
+
 // Correspondence maps of 2048 pixels per workgroup (slg_decode): col/row int32, mask uint8.
 __global__ __launch_bounds__(kBlock) void decode_maps_kernel(MainParams p) {
   const int64_t px0 = int64_t(blockIdx.x) * kMapsPx + int64_t(threadIdx.x) * kPx;
@@ -1513,7 +1579,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       uint64_t* st = p.states + int64_t(s) * tiles;
       uint64_t excl;
       int ht;
-      while (!lookback_try<PROF>(p, st, tile, agg, excl, ht, rec[4], rec[5])) {
+      while (!(SLG_SCALAR_LB ? lookback_scalar<PROF>(p, st, tile, agg, excl, ht, rec[4], rec[5])
+                             : lookback_try<PROF>(p, st, tile, agg, excl, ht, rec[4], rec[5]))) {
         // a predecessor has not published for long (it may not be dispatched yet): publish
         // its aggregate for it, computed by this wave, and look back again
         const int hagg = tile_keep_count_wave<ROW_MODE, SRC_FRAMES, RAYS>(p, ht, s);
