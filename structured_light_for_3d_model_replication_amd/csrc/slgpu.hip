@@ -663,25 +663,59 @@ struct MainParams {
                            // (kHelpAfter; env SLG_HELP_AFTER=0 forces the helper path in tests)
 };
 
-// code of pixel k (0..7) from the packed accumulators
-__device__ inline int unpack_code(const uint32_t (&acc)[4], int k) {
-  const uint32_t a = acc[((k >> 2) << 1) | (k & 1)];
-  return int((a >> (16 * ((k >> 1) & 1))) & 0xffffu);
-}
-
 // ------------------------------------------------------------------ decode (shared by the kernels)
-__device__ inline void acc_pair(uint32_t (&acc)[4], uint2 pv, uint2 iv) {
+// Bit planes of 4 pixels accumulate one byte per pixel: plane b's compare mask (bit 7 of each
+// byte: pattern > inverse) enters at bit 7 while the earlier planes shift down, two VALU ops per
+// word per plane.  Planes 0-7 go to word A, planes 8-14 to word B.  After n planes, bit-reversing
+// the word (v_bfrev: bits within a byte AND the byte order) leaves pixel k's code MSB-first in
+// byte 3-k: A' byte = code >> m, B' byte = code & (2^m - 1), m = max(n - 8, 0).
+struct PlaneAcc {
+  uint32_t a[2], b[2];       // [pixels 0-3, 4-7]
+};
+
+__device__ inline void acc_plane(uint32_t& w, uint32_t m) { w = (w >> 1) | (m & 0x80808080u); }
+
+template <bool HI>
+__device__ inline void acc_pair(PlaneAcc& q, uint2 pv, uint2 iv) {
   const uint32_t m0 = gt_u8x4(pv.x, iv.x);
   const uint32_t m1 = gt_u8x4(pv.y, iv.y);
-  acc[0] = (acc[0] << 1) | ((m0 >> 7) & 0x00010001u);
-  acc[1] = (acc[1] << 1) | ((m0 >> 15) & 0x00010001u);
-  acc[2] = (acc[2] << 1) | ((m1 >> 7) & 0x00010001u);
-  acc[3] = (acc[3] << 1) | ((m1 >> 15) & 0x00010001u);
+  if (HI) { acc_plane(q.b[0], m0); acc_plane(q.b[1], m1); }
+  else { acc_plane(q.a[0], m0); acc_plane(q.a[1], m1); }
+}
+
+// The n-plane Gray codes of the lane's 8 pixels as two per word (16-bit halves), converted
+// like gray2bin_x2(code << pre) << post: w[2h] = pixels (4h, 4h+2) in (high, low) halves,
+// w[2h+1] = pixels (4h+1, 4h+3).
+__device__ inline void acc_codes(const PlaneAcc& q, int n, int pre, int post, uint32_t (&w)[4]) {
+  const int m = n > 8 ? n - 8 : 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t A = __builtin_bitreverse32(q.a[h]), B = __builtin_bitreverse32(q.b[h]);
+    const uint32_t hi = (((A >> 8) & 0x00ff00ffu) << m) | ((B >> 8) & 0x00ff00ffu);
+    const uint32_t lo = ((A & 0x00ff00ffu) << m) | (B & 0x00ff00ffu);
+    w[2 * h] = gray2bin_x2(hi << pre) << post;
+    w[2 * h + 1] = gray2bin_x2(lo << pre) << post;
+  }
+}
+
+// code of pixel k (0..7) from acc_codes' words
+__device__ inline int unpack_code(const uint32_t (&w)[4], int k) {
+  const uint32_t a = w[((k >> 2) << 1) | (k & 1)];
+  return int((a >> (16 * (1 - ((k >> 1) & 1)))) & 0xffffu);
+}
+
+// A wave-uniform 64-bit value pinned to SGPRs: the compiler cannot fold a lane offset into it
+// first, so frame f's address is (frames + lane offset) + one scalar term -- one VALU add per
+// load instead of a 64-bit vector multiply-add.
+__device__ inline int64_t sgpr64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(uint64_t(v)));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(uint64_t(v) >> 32));
+  return int64_t((uint64_t(hi) << 32) | lo);
 }
 
 // 8 frame bytes at pixel lp (clamped in-bounds by the caller; rows are padded to >= 8 px).
 __device__ inline uint2 ld_frame8(const MainParams& p, int frame, int64_t lp) {
-  return ld_once8(p.frames + int64_t(frame) * p.stride + lp);
+  return ld_once8(p.frames + sgpr64(int64_t(frame) * p.stride) + uint32_t(lp));
 }
 
 // Decode the 8 pixels of one lane: mask bits + column / row codes.  Frame loads of both axes
@@ -698,7 +732,7 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
     const int64_t lp = px0 < p.n_px ? px0 : 0;
     const uint2 w = ld_frame8(p, 0, lp);
     const uint2 bl = ld_frame8(p, 1, lp);
-    uint32_t ac[4] = {0, 0, 0, 0}, ar[4] = {0, 0, 0, 0};
+    PlaneAcc qc = {{0, 0}, {0, 0}}, qr = {{0, 0}, {0, 0}};
     const int np_r = ROW_MODE != 0 ? p.row_pairs : 0;
     // compile-time trip count (kMaxBits pairs max), fully unrolled: only forward, wave-uniform
     // branches remain, so the loads of a batch stay in flight together (no vmcnt(0) per load)
@@ -719,16 +753,20 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
         }
 #pragma unroll
       for (int g = 0; g < kBatch; ++g)
-        if (b0 + g < p.col_pairs) acc_pair(ac, cp[g], ci[g]);
+        if (b0 + g < p.col_pairs) {
+          if (b0 + g < 8) acc_pair<false>(qc, cp[g], ci[g]);
+          else acc_pair<true>(qc, cp[g], ci[g]);
+        }
 #pragma unroll
       for (int g = 0; g < kBatch; ++g)
-        if (b0 + g < np_r) acc_pair(ar, rp[g], ri[g]);
+        if (b0 + g < np_r) {
+          if (b0 + g < 8) acc_pair<false>(qr, rp[g], ri[g]);
+          else acc_pair<true>(qr, rp[g], ri[g]);
+        }
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ac[j] = gray2bin_x2(ac[j] << p.col_pre) << p.col_post;
-      ar[j] = gray2bin_x2(ar[j] << p.row_pre) << p.row_post;
-    }
+    uint32_t ac[4], ar[4];
+    acc_codes(qc, p.col_pairs, p.col_pre, p.col_post, ac);
+    acc_codes(qr, np_r, p.row_pre, p.row_post, ar);
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
       const int wv = ((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 0xff;
