@@ -1430,6 +1430,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   __shared__ __attribute__((aligned(16))) uint32_t s_uv[kTilePx];     // its pixel coordinates u | v << 16
   __shared__ int s_wtot[kB / 64];
   __shared__ int s_cnt[NS][kIt][kB / 64];  // kept points per (round, wave)
+  __shared__ int s_loc[NS][kIt][kB / 64];  // their exclusive offsets within the tile (phase C)
   __shared__ uint64_t s_excl[NS];
   // after phase B the item arrays are dead (only s_bgr is read again): the carried batch's
   // nibble planes and histograms reuse them, so the workgroup needs 24 KB of LDS, not 35
@@ -1612,8 +1613,18 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   if (wave == 0) {
 #pragma unroll 1
     for (int s = 0; s < NS; ++s) {
-      int agg = 0;
-      for (int q = 0; q < kIt * (kB / 64); ++q) agg += (&s_cnt[s][0][0])[q];
+      // one lane per (round, wave) count: the tile aggregate and, for phase D, each (round,
+      // wave)'s offset within the tile -- one wave-wide scan instead of per-round sums later
+      static_assert(kIt * (kB / 64) == 64, "one lane per (round, wave)");
+      const int cnt = (&s_cnt[s][0][0])[lane];
+      int incl = cnt;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      (&s_loc[s][0][0])[lane] = incl - cnt;
+      const int agg = __shfl(incl, 63);
       uint64_t* st = p.states + int64_t(s) * tiles;
       uint64_t excl;
       int ht;
@@ -1647,20 +1658,13 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    int64_t base = int64_t(s_excl[s]);
+    const int64_t base = int64_t(s_excl[s]);
     XT* gx = reinterpret_cast<XT*>(s == 0 ? p.xyz : p.scratch_xyz);
     uint8_t* gb = s == 0 ? p.bgr : p.scratch_bgr;
 #pragma unroll
     for (int i = 0; i < kIt; ++i) {
-      int before = 0, round = 0;
-#pragma unroll
-      for (int w = 0; w < kB / 64; ++w) {
-        const int c = s_cnt[s][i][w];
-        before += w < wave ? c : 0;
-        round += c;
-      }
       if ((km[s][i] >> lane) & 1ull) {
-        const int64_t q = base + before + __popcll(km[s][i] & lt);
+        const int64_t q = base + s_loc[s][i][wave] + __popcll(km[s][i] & lt);
         const uint32_t c = s_bgr[tid + kB * i];
         bool packed = false;
         if constexpr (PROF && sizeof(XT) == 4) {     // PROF bit 8: one 16-byte {x, y, z, bgr} record
@@ -1679,7 +1683,6 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
           gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
         }
       }
-      base += round;
     }
   }
   if (prof) {
