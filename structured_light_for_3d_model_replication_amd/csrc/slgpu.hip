@@ -1105,7 +1105,10 @@ __device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int ag
 __device__ inline void ld_state8_scalar(const uint64_t* p, uint64_t (&v)[8]) {
   typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
   u32x16 r;
-  asm volatile("s_load_dwordx16 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
+  const uint64_t a = reinterpret_cast<uint64_t>(p);   // uniform: pinned to SGPRs for the "s" operand
+  const uint64_t sa = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(a >> 32))) << 32) |
+                      __builtin_amdgcn_readfirstlane(uint32_t(a));
+  asm volatile("s_load_dwordx16 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(sa) : "memory");
 #pragma unroll
   for (int k = 0; k < 8; ++k) v[k] = uint64_t(r[2 * k]) | (uint64_t(r[2 * k + 1]) << 32);
 }
