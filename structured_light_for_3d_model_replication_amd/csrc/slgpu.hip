@@ -1106,8 +1106,9 @@ __device__ inline void ld_state8_scalar(const uint64_t* p, uint64_t (&v)[8]) {
   typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
   u32x16 r;
   const uint64_t a = reinterpret_cast<uint64_t>(p);   // uniform: pinned to SGPRs for the "s" operand
-  const uint64_t sa = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(a >> 32))) << 32) |
-                      __builtin_amdgcn_readfirstlane(uint32_t(a));
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(a));          // (the builtin returns int:
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(a >> 32));    //  widen only as uint32)
+  const uint64_t sa = (uint64_t(hi) << 32) | lo;
   asm volatile("s_load_dwordx16 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(sa) : "memory");
 #pragma unroll
   for (int k = 0; k < 8; ++k) v[k] = uint64_t(r[2 * k]) | (uint64_t(r[2 * k + 1]) << 32);
