@@ -102,6 +102,9 @@ __device__ inline void st_state(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifndef SLG_FRAME_BUFFER_LOADS
+#define SLG_FRAME_BUFFER_LOADS 1           // frame loads as buffer loads (scalar base, 32-bit lane offset)
+#endif
 #ifndef SLG_NT_LOADS
 #define SLG_NT_LOADS 1                     // frames / texture are read once: non-temporal loads
 #endif
@@ -130,8 +133,12 @@ __device__ inline int wave_min_i(int x) {
 
 // Per-byte unsigned p > i on 4 packed bytes: 0x80 in every byte lane where p > i.
 __device__ inline uint32_t gt_u8x4(uint32_t p, uint32_t i) {
-  const uint32_t d = (i | 0x80808080u) - (p & 0x7f7f7f7fu);   // hi bit: low7(i) >= low7(p)
-  return ((p & ~i) | (~(p ^ i) & ~d)) & 0x80808080u;
+  // per byte p > i in bit 7 (other bits garbage: callers mask with 0x80808080):
+  // f(p, i, d) = (p & ~i) | (~(p ^ i) & ~d), d = (i | 0x80) - (p & 0x7f) per byte, one v_bitop3
+  const uint32_t d = (i | 0x80808080u) - (p & 0x7f7f7f7fu);
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x71" : "=v"(r) : "v"(p), "v"(i), "v"(d));
+  return r;
 }
 
 // Gray -> binary on two packed 16-bit lanes (values < 2^15): prefix XOR from the top.
@@ -714,8 +721,17 @@ __device__ inline int64_t sgpr64(int64_t v) {
 }
 
 // 8 frame bytes at pixel lp (clamped in-bounds by the caller; rows are padded to >= 8 px).
+// As a buffer load: the frame's base lives in a scalar resource descriptor and the lane offset
+// is a 32-bit VGPR (buffer_load_dwordx2 ... offen nt), so the address costs no VALU at all.
 __device__ inline uint2 ld_frame8(const MainParams& p, int frame, int64_t lp) {
+#if SLG_FRAME_BUFFER_LOADS
+  const uint8_t* base = p.frames + sgpr64(int64_t(frame) * p.stride);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0xffffffff, 0x00020000);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, uint32_t(lp), 0, SLG_NT_LOADS ? 2 : 0);   // aux 2: nt
+  return make_uint2(v[0], v[1]);
+#else
   return ld_once8(p.frames + sgpr64(int64_t(frame) * p.stride) + uint32_t(lp));
+#endif
 }
 
 // Decode the 8 pixels of one lane: mask bits + column / row codes.  Frame loads of both axes
