@@ -711,6 +711,13 @@ __device__ inline int unpack_code(const uint32_t (&w)[4], int k) {
   return int((a >> (16 * (1 - ((k >> 1) & 1)))) & 0xffffu);
 }
 
+// 8 once-read bytes at base + off as a buffer load (scalar descriptor, 32-bit lane offset).
+__device__ inline uint2 ld_once8_buf(const uint8_t* base, uint32_t off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0xffffffff, 0x00020000);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, SLG_NT_LOADS ? 2 : 0);   // aux 2: nt
+  return make_uint2(v[0], v[1]);
+}
+
 // A wave-uniform 64-bit value pinned to SGPRs: the compiler cannot fold a lane offset into it
 // first, so frame f's address is (frames + lane offset) + one scalar term -- one VALU add per
 // load instead of a 64-bit vector multiply-add.
@@ -1314,8 +1321,8 @@ __device__ inline void hist_next_load(const uint8_t* white, const uint8_t* black
   wq = make_uint2(0, 0);
   bq = make_uint2(0, 0);
   if (o < n_px) {                            // frames readable to round_up(n, 8)
-    wq = ld_once8(white + o);
-    bq = ld_once8(black + o);
+    wq = ld_once8_buf(white, uint32_t(o));     // o < n_px < 2^31
+    bq = ld_once8_buf(black, uint32_t(o));
   }
 }
 
@@ -1503,8 +1510,9 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   {
     uint32_t tex[6] = {0, 0, 0, 0, 0, 0};
     if (!tail) {
-      const uint8_t* tq = p.texture + px0 * 3;
-      const uint2 t0 = ld_once8(tq), t1 = ld_once8(tq + 8), t2 = ld_once8(tq + 16);
+      const uint32_t tq = uint32_t(px0) * 3u;     // n_px * 3 < 2^32 (host: slg_capture checks)
+      const uint2 t0 = ld_once8_buf(p.texture, tq), t1 = ld_once8_buf(p.texture, tq + 8u),
+                  t2 = ld_once8_buf(p.texture, tq + 16u);
       tex[0] = t0.x; tex[1] = t0.y; tex[2] = t1.x; tex[3] = t1.y; tex[4] = t2.x; tex[5] = t2.y;
     } else {
       for (int k = 0; k < 3 * kPx; ++k)
@@ -1872,6 +1880,8 @@ int check_capture(const slg_capture* cap) {
   if (cap->height < 1 || cap->width < 1) return fail(SLG_ERR_INVALID, "bad image size %dx%d", cap->width, cap->height);
   const int64_t n_px = int64_t(cap->height) * cap->width;
   if (n_px >= (int64_t(1) << 31)) return fail(SLG_ERR_UNSUPPORTED, "image larger than 2^31 pixels");
+  if (n_px * 3 + 64 >= (int64_t(1) << 32))        // texture reads take 32-bit byte offsets
+    return fail(SLG_ERR_UNSUPPORTED, "image larger than 1.43e9 pixels");
   if (cap->height > 65535 || cap->width > 65535) return fail(SLG_ERR_UNSUPPORTED, "image side above 65535 pixels");
   if (cap->frame_stride < ((n_px + 7) & ~int64_t(7)) || (cap->frame_stride & 7))
     return fail(SLG_ERR_INVALID, "frame_stride must be >= round_up(H*W, 8) and a multiple of 8");
