@@ -732,9 +732,11 @@ __device__ inline int64_t sgpr64(int64_t v) {
 // is a 32-bit VGPR (buffer_load_dwordx2 ... offen nt), so the address costs no VALU at all.
 __device__ inline uint2 ld_frame8(const MainParams& p, int frame, int64_t lp) {
 #if SLG_FRAME_BUFFER_LOADS
-  const uint8_t* base = p.frames + sgpr64(int64_t(frame) * p.stride);
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, 0xffffffff, 0x00020000);
-  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, uint32_t(lp), 0, SLG_NT_LOADS ? 2 : 0);   // aux 2: nt
+  // one descriptor for the whole stack, the frame's offset in the scalar soffset (a capture's
+  // frames span < 4 GiB: check_capture)
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.frames), 0, 0xffffffff, 0x00020000);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, uint32_t(lp), uint32_t(frame) * uint32_t(p.stride),
+                                                      SLG_NT_LOADS ? 2 : 0);   // aux 2: nt
   return make_uint2(v[0], v[1]);
 #else
   return ld_once8(p.frames + sgpr64(int64_t(frame) * p.stride) + uint32_t(lp));
@@ -1886,6 +1888,8 @@ int check_capture(const slg_capture* cap) {
   if (cap->frame_stride < ((n_px + 7) & ~int64_t(7)) || (cap->frame_stride & 7))
     return fail(SLG_ERR_INVALID, "frame_stride must be >= round_up(H*W, 8) and a multiple of 8");
   if (reinterpret_cast<uintptr_t>(cap->frames) & 7) return fail(SLG_ERR_INVALID, "frames must be 8-byte aligned");
+  if (int64_t(cap->n_frames > 0 ? cap->n_frames : 0) * cap->frame_stride >= (int64_t(1) << 32))
+    return fail(SLG_ERR_UNSUPPORTED, "frame stack larger than 4 GiB");   // 32-bit buffer offsets
   return SLG_OK;
 }
 
