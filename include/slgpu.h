@@ -76,6 +76,8 @@ extern "C" {
 #define SLG_RAYS_TABLE 0         /* gather Nc[:, idx] (processing.py:143-144) */
 #define SLG_RAYS_PINHOLE 1       /* recompute from cam_K (processing.py:145-156) */
 
+/* Limits (SLG_ERR_UNSUPPORTED otherwise): height*width < 1.43e9 and n_frames*frame_stride
+ * < 4 GiB -- the kernels address frames and texture with 32-bit buffer offsets. */
 typedef struct slg_capture {
   const uint8_t *frames;   /* device, [n_frames][frame_stride] */
   int64_t frame_stride;    /* bytes between frames (>= round_up(height*width, 8), % 8 == 0) */
