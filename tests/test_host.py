@@ -39,6 +39,32 @@ def test_library_loads_and_exports_every_header_symbol():
     assert r["ws"] > 1920 * 1080 * 27
 
 
+def test_capture_limits_rejected_before_any_launch():
+    """The kernels address frames and texture with 32-bit buffer offsets (include/slgpu.h): a
+    frame stack of 4 GiB or more, or an image of 1.43e9 pixels or more, is refused by the C ABI's
+    argument check, before anything touches the GPU (fake, never dereferenced pointers)."""
+    code = (
+        "import ctypes, json\n"
+        f"import {PKG}._native as N\n"
+        "L = N.lib()\n"
+        "dp = N.DecodeParams(proj_cols=1920, proj_rows=1080, n_sets_col=11, n_sets_row=11)\n"
+        "out = {}\n"
+        "for tag, h, w, stride, nf in (('stack', 1080, 1920, 1 << 29, 8), ('pixels', 40000, 40000, 1600000000, 4),\n"
+        "                              ('ok_stack', 1080, 1920, 1 << 29, 7)):\n"
+        "    cap = N.Capture(frames=4096, frame_stride=stride, n_frames=nf, height=h, width=w, texture=4096)\n"
+        "    rc = L.slg_decode_stats(ctypes.byref(cap), ctypes.byref(dp), None, None)\n"
+        "    out[tag] = [rc, L.slg_last_error().decode()]\n"
+        "print(json.dumps(out))\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, check=True)
+    import json
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    from structured_light_for_3d_model_replication_amd import _native as N
+    assert res["stack"][0] == N.SLG_ERR_UNSUPPORTED and "4 GiB" in res["stack"][1]
+    assert res["pixels"][0] == N.SLG_ERR_UNSUPPORTED and "1.43e9" in res["pixels"][1]
+    # 7 x 512 MiB passes the capture check and stops at the NULL workspace instead
+    assert res["ok_stack"][0] == N.SLG_ERR_INVALID and "NULL" in res["ok_stack"][1]
+
+
 def test_exports_match_ctypes_table():
     from structured_light_for_3d_model_replication_amd import _native as N
     assert sorted(N.EXPORTS) == header_exports()
