@@ -1242,6 +1242,9 @@ constexpr int kMaxViews = 16;
 #ifndef SLG_TRI_GROUP
 #define SLG_TRI_GROUP 4                    // phase B: rounds (items per lane) whose gathers are in flight together
 #endif
+#ifndef SLG_HN_OWN_LDS
+#define SLG_HN_OWN_LDS 1                   // carried-histogram staging in its own LDS (no extra barrier)
+#endif
 #ifndef SLG_M3_WAVES
 #define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
 #endif
@@ -1461,11 +1464,18 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   __shared__ int s_cnt[NS][kIt][kB / 64];  // kept points per (round, wave)
   __shared__ int s_loc[NS][kIt][kB / 64];  // their exclusive offsets within the tile (phase C)
   __shared__ uint64_t s_excl[NS];
+#if SLG_HN_OWN_LDS
+  // the carried batch's nibble planes and histograms in LDS of their own (67 KB per workgroup,
+  // two per CU): each wave stages its lane data as soon as phase A ends, no extra barrier
+  __shared__ uint2 s_hstage[(kB / 64) * 256];                         // [wave][4 planes][64 lanes]
+  __shared__ uint32_t s_hn[512];                                      // histograms
+#else
   // after phase B the item arrays are dead (only s_bgr is read again): the carried batch's
   // nibble planes and histograms reuse them, so the workgroup needs 24 KB of LDS, not 35
   uint2* const s_hstage = reinterpret_cast<uint2*>(s_uv);            // [wave][4 planes][64 lanes]
   uint32_t* const s_hn = s_code;                                      // [512] histograms
   static_assert((kB / 64) * 256 * sizeof(uint2) <= sizeof(s_uv) && 512 <= kTilePx, "aliases");
+#endif
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = int(P.c.n_tiles);
@@ -1542,6 +1552,12 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   __syncthreads();
 
   stamp(0);
+#if SLG_HN_OWN_LDS
+  if (hn) {                                          // block-uniform; counted in phase C
+    for (int i = tid; i < 512; i += kB) s_hn[i] = 0;
+    hist_next_stage(hn_w, hn_b, p.n_px, px0, s_hstage);
+  }
+#endif
   // ------------------------------------------------------------ B: triangulate, balanced
   // Item m = tid + kB * i: every wave gets an equal share of the tile's valid pixels.
   // Points stay in registers across the look-back (recomputing them after it instead frees
@@ -1631,11 +1647,13 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       }
     }
   }
+#if !SLG_HN_OWN_LDS
   if (hn) {                                          // block-uniform
     __syncthreads();                                 // every wave is past its phase-B item reads
     for (int i = tid; i < 512; i += kB) s_hn[i] = 0;
     hist_next_stage(hn_w, hn_b, p.n_px, px0, s_hstage);
   }
+#endif
   __syncthreads();
 
   stamp(1);
