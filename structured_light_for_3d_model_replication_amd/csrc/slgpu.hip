@@ -1242,9 +1242,6 @@ constexpr int kMaxViews = 16;
 #ifndef SLG_TRI_GROUP
 #define SLG_TRI_GROUP 4                    // phase B: rounds (items per lane) whose gathers are in flight together
 #endif
-#ifndef SLG_HN_OWN_LDS
-#define SLG_HN_OWN_LDS 1                   // carried-histogram staging in its own LDS (no extra barrier)
-#endif
 #ifndef SLG_M3_WAVES
 #define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
 #endif
@@ -1403,8 +1400,8 @@ __device__ inline int2 block_scan(int x, int* s_wtot) {
 // loads and fp64 chains are independent, so their plane gathers are in flight together.
 // tri_rounds: i is a compile-time multiple of G (the unrolled group loop); tri_rounds_at: any i.
 template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NOG = 0, int NP = 0>
-__device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, const uint32_t* s_code,
-                                     const uint32_t* s_uv, XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
+__device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, const uint2* s_item,
+                                     XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
   const int tid = threadIdx.x;
   TriOut o[G];
   TriPlanes pl[G];
@@ -1415,7 +1412,8 @@ __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, co
   for (int h = 0; h < G; ++h) {                    // the G items' plane gathers, all in flight ...
     const int m = tid + kTileBlock * (i + h);
     in[h] = m < n_items;
-    const uint32_t sc = s_code[m], suv = s_uv[m];   // m < kTilePx; garbage past n_items masked
+    const uint2 it = s_item[m];                     // m < kTilePx; garbage past n_items masked
+    const uint32_t sc = it.x, suv = it.y;
     const uint32_t code = in[h] ? sc : 0u;
     uvs[h] = in[h] ? suv : 0u;
     pl[h] = tri_planes<ROW_MODE, NOG, NP>(p, code);
@@ -1444,9 +1442,9 @@ __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, co
 }
 
 template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NOG = 0, int NP = 0>
-__device__ inline void tri_rounds(const MainParams& p, int i, int n_items, const uint32_t* s_code,
-                                  const uint32_t* s_uv, XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
-  tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_code, s_uv, pts, km);
+__device__ inline void tri_rounds(const MainParams& p, int i, int n_items, const uint2* s_item,
+                                  XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
+  tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_item, pts, km);
 }
 
 // PROF: the profiling instance (SLG_DBG set): honours the ablation bits of MainParams::dbg and
@@ -1457,25 +1455,17 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   constexpr int NS = ROW_MODE == 2 ? 2 : 1;
   constexpr int kB = kTileBlock;
   constexpr int kIt = kTilePx / kB;        // 8 item rounds of one workgroup at most
-  __shared__ __attribute__((aligned(16))) uint32_t s_code[kTilePx];   // valid item: col | row << 16
+  __shared__ __attribute__((aligned(16))) uint2 s_item[kTilePx];     // valid item: (col | row << 16, u | v << 16)
   __shared__ uint32_t s_bgr[kTilePx];      // its BGR (24 bits)
-  __shared__ __attribute__((aligned(16))) uint32_t s_uv[kTilePx];     // its pixel coordinates u | v << 16
   __shared__ int s_wtot[kB / 64];
   __shared__ int s_cnt[NS][kIt][kB / 64];  // kept points per (round, wave)
   __shared__ int s_loc[NS][kIt][kB / 64];  // their exclusive offsets within the tile (phase C)
   __shared__ uint64_t s_excl[NS];
-#if SLG_HN_OWN_LDS
-  // the carried batch's nibble planes and histograms in LDS of their own (67 KB per workgroup,
+  // the carried batch's nibble planes and histograms in LDS of their own (68 KB per workgroup,
   // two per CU): each wave stages its lane data as soon as phase A ends, no extra barrier
+  // (289.7 vs 291.6 us per launch against aliasing the item arrays after phase B)
   __shared__ uint2 s_hstage[(kB / 64) * 256];                         // [wave][4 planes][64 lanes]
   __shared__ uint32_t s_hn[512];                                      // histograms
-#else
-  // after phase B the item arrays are dead (only s_bgr is read again): the carried batch's
-  // nibble planes and histograms reuse them, so the workgroup needs 24 KB of LDS, not 35
-  uint2* const s_hstage = reinterpret_cast<uint2*>(s_uv);            // [wave][4 planes][64 lanes]
-  uint32_t* const s_hn = s_code;                                      // [512] histograms
-  static_assert((kB / 64) * 256 * sizeof(uint2) <= sizeof(s_uv) && 512 <= kTilePx, "aliases");
-#endif
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = int(P.c.n_tiles);
@@ -1483,7 +1473,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   if (int(blockIdx.x) < n_fin_wg) {
     const int fv = int(blockIdx.x) / P.fin_blocks;
     otsu_from_parts(P.fin[fv].parts, P.fin[fv].ws, tiles, P.c.n_px, P.n_state_words, P.pad_zero,
-                    int(blockIdx.x) - fv * P.fin_blocks, P.fin_blocks, s_code, s_bgr);
+                    int(blockIdx.x) - fv * P.fin_blocks, P.fin_blocks, reinterpret_cast<uint32_t*>(s_item), s_bgr);
     return;
   }
   const int bid = int(blockIdx.x) - n_fin_wg;
@@ -1541,9 +1531,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
       if (valid & (1u << k)) {
-        s_code[m] = pack_code<ROW_MODE>(p, col[k], row[k]);
+        s_item[m] = make_uint2(pack_code<ROW_MODE>(p, col[k], row[k]), uint32_t(u) | (uint32_t(v) << 16));
         s_bgr[m] = bgr_of(tex, k);
-        s_uv[m] = uint32_t(u) | (uint32_t(v) << 16);
         ++m;
       }
       if (++u == p.width) { u = 0; ++v; }
@@ -1552,12 +1541,10 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   __syncthreads();
 
   stamp(0);
-#if SLG_HN_OWN_LDS
   if (hn) {                                          // block-uniform; counted in phase C
     for (int i = tid; i < 512; i += kB) s_hn[i] = 0;
     hist_next_stage(hn_w, hn_b, p.n_px, px0, s_hstage);
   }
-#endif
   // ------------------------------------------------------------ B: triangulate, balanced
   // Item m = tid + kB * i: every wave gets an equal share of the tile's valid pixels.
   // Points stay in registers across the look-back (recomputing them after it instead frees
@@ -1579,15 +1566,15 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
 #pragma unroll
       for (int g = 0; g + SLG_TRI_GROUP <= kIt; g += SLG_TRI_GROUP)
         if (i + SLG_TRI_GROUP <= rounds) {
-          tri_rounds<SLG_TRI_GROUP, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, g, n_items, s_code, s_uv, pts, km);
+          tri_rounds<SLG_TRI_GROUP, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, g, n_items, s_item, pts, km);
           i = g + SLG_TRI_GROUP;
         }
       if (SLG_TRI_GROUP > 2 && i + 2 <= rounds) {
-        tri_rounds_at<2, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_code, s_uv, pts, km);
+        tri_rounds_at<2, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_item, pts, km);
         i += 2;
       }
       if (i < rounds) {
-        tri_rounds_at<1, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_code, s_uv, pts, km);
+        tri_rounds_at<1, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_item, pts, km);
         i += 1;
       }
     };
@@ -1624,7 +1611,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       if (i * kB < n_items) {                          // block-uniform
         const int m = tid + kB * i;
         const bool in = m < n_items;
-        const uint32_t sc = s_code[m], suv = s_uv[m];   // read unconditionally (m < kTilePx) ...
+        const uint2 it = s_item[m];                     // read unconditionally (m < kTilePx) ...
+        const uint32_t sc = it.x, suv = it.y;
         const uint32_t code = in ? sc : 0u, uv = in ? suv : 0u;   // ... garbage past n_items masked
         const int u = int(uv & 0xffffu), v = int(uv >> 16);
         uint32_t keep;
@@ -1647,13 +1635,6 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       }
     }
   }
-#if !SLG_HN_OWN_LDS
-  if (hn) {                                          // block-uniform
-    __syncthreads();                                 // every wave is past its phase-B item reads
-    for (int i = tid; i < 512; i += kB) s_hn[i] = 0;
-    hist_next_stage(hn_w, hn_b, p.n_px, px0, s_hstage);
-  }
-#endif
   __syncthreads();
 
   stamp(1);
