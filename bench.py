@@ -195,10 +195,18 @@ def main():
         log(f"[rank 0] cpu baseline {cpu['value']} Mpts/s on {cpu['cores']} processes "
             f"({cpu['single_process_value']} on 1) in {time.perf_counter() - t:.1f}s")
 
+    # Rehearsal knobs for the multi-rank path on a one-GPU box (never set by the driver):
+    # SLG_BENCH_DEVICE pins every rank to one device, SLG_BENCH_BACKEND=gloo replaces RCCL.
+    if os.environ.get("SLG_BENCH_DEVICE"):
+        local = int(os.environ["SLG_BENCH_DEVICE"])
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("SLG_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     from structured_light_for_3d_model_replication_amd import engine as E
 
     cfg = E.DecodeConfig(PW, PH, NC, NR, "otsu")
