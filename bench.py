@@ -140,6 +140,9 @@ def load_traffic_per_view():
         return None
 
 
+RESULT_OUT = sys.stdout          # main() points it at the original stdout
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -163,11 +166,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     args = ap.parse_args()
+    # stdout carries exactly ONE line, the JSON result: runtime banners that native libraries
+    # print to fd 1 (RCCL's version block, gloo's peer lines) go to stderr with the logs
+    global RESULT_OUT
+    RESULT_OUT = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     wl = CONFIGS[args.config]
     for k in ("views", "copies", "batch"):
         if getattr(args, k) is None:
             setattr(args, k, wl[k])
     if args.config == "c3":
+        args.result_out = RESULT_OUT
         import bench_c3
         return bench_c3.main(args, wl)
 
@@ -396,7 +406,7 @@ def main():
             "cpu_baseline": cpu,
             "verify": verify,
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=RESULT_OUT, flush=True)
     if world > 1:
         dist.destroy_process_group()
 

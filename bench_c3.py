@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 import time
 
 import bench
@@ -200,7 +201,7 @@ def main(args, wl):
             "cpu_baseline": cpu,
             "verify": verify,
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=getattr(args, "result_out", None) or sys.stdout, flush=True)
     gather.close()
     if world > 1:
         dist.destroy_process_group()
