@@ -1422,6 +1422,13 @@ __device__ inline int2 block_scan(int x, int* s_wtot) {
   return make_int2(off + incl - x, tot);
 }
 
+// LDS slots of compacted item m: phase A writes lane L's items at m = prefix(L) + j, a stride of
+// up to 8 items between neighbouring lanes (16 words for the 8-byte records: 16 lanes per
+// bank); one pad slot per 16 records (per 8 BGR words) makes that stride odd in words.
+constexpr int kItemSlots = kTilePx + kTilePx / 16, kBgrSlots = kTilePx + kTilePx / 8;
+__device__ inline int item_slot(int m) { return m + (m >> 4); }
+__device__ inline int bgr_slot(int m) { return m + (m >> 3); }
+
 // Phase B of main3 for rounds [i, i + G) (item m = tid + 256 * round), FAST path: the G items'
 // loads and fp64 chains are independent, so their plane gathers are in flight together.
 // tri_rounds: i is a compile-time multiple of G (the unrolled group loop); tri_rounds_at: any i.
@@ -1438,7 +1445,7 @@ __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, co
   for (int h = 0; h < G; ++h) {                    // the G items' plane gathers, all in flight ...
     const int m = tid + kTileBlock * (i + h);
     in[h] = m < n_items;
-    const uint2 it = s_item[m];                     // m < kTilePx; garbage past n_items masked
+    const uint2 it = s_item[item_slot(m)];          // m < kTilePx; garbage past n_items masked
     const uint32_t sc = it.x, suv = it.y;
     const uint32_t code = in[h] ? sc : 0u;
     uvs[h] = in[h] ? suv : 0u;
@@ -1481,8 +1488,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   constexpr int NS = ROW_MODE == 2 ? 2 : 1;
   constexpr int kB = kTileBlock;
   constexpr int kIt = kTilePx / kB;        // 8 item rounds of one workgroup at most
-  __shared__ __attribute__((aligned(16))) uint2 s_item[kTilePx];     // valid item: (col | row << 16, u | v << 16)
-  __shared__ uint32_t s_bgr[kTilePx];      // its BGR (24 bits)
+  __shared__ __attribute__((aligned(16))) uint2 s_item[kItemSlots];  // valid item: (col | row << 16, u | v << 16)
+  __shared__ uint32_t s_bgr[kBgrSlots];    // its BGR (24 bits)
   __shared__ int s_wtot[kB / 64];
   __shared__ int s_cnt[NS][kIt][kB / 64];  // kept points per (round, wave)
   __shared__ int s_loc[NS][kIt][kB / 64];  // their exclusive offsets within the tile (phase C)
@@ -1557,8 +1564,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
       if (valid & (1u << k)) {
-        s_item[m] = make_uint2(pack_code<ROW_MODE>(p, col[k], row[k]), uint32_t(u) | (uint32_t(v) << 16));
-        s_bgr[m] = bgr_of(tex, k);
+        s_item[item_slot(m)] = make_uint2(pack_code<ROW_MODE>(p, col[k], row[k]), uint32_t(u) | (uint32_t(v) << 16));
+        s_bgr[bgr_slot(m)] = bgr_of(tex, k);
         ++m;
       }
       if (++u == p.width) { u = 0; ++v; }
@@ -1637,7 +1644,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       if (i * kB < n_items) {                          // block-uniform
         const int m = tid + kB * i;
         const bool in = m < n_items;
-        const uint2 it = s_item[m];                     // read unconditionally (m < kTilePx) ...
+        const uint2 it = s_item[item_slot(m)];          // read unconditionally (m < kTilePx) ...
         const uint32_t sc = it.x, suv = it.y;
         const uint32_t code = in ? sc : 0u, uv = in ? suv : 0u;   // ... garbage past n_items masked
         const int u = int(uv & 0xffffu), v = int(uv >> 16);
@@ -1720,7 +1727,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     for (int i = 0; i < kIt; ++i) {
       if ((km[s][i] >> lane) & 1ull) {
         const int64_t q = base + s_loc[s][i][wave] + __popcll(km[s][i] & lt);
-        const uint32_t c = s_bgr[tid + kB * i];
+        const uint32_t c = s_bgr[bgr_slot(tid + kB * i)];
         bool packed = false;
         if constexpr (PROF && sizeof(XT) == 4) {     // PROF bit 8: one 16-byte {x, y, z, bgr} record
           if (p.dbg & 256) {
