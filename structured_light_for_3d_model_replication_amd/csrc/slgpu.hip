@@ -1425,9 +1425,15 @@ __device__ inline int2 block_scan(int x, int* s_wtot) {
 // LDS slots of compacted item m: phase A writes lane L's items at m = prefix(L) + j, a stride of
 // up to 8 items between neighbouring lanes (16 words for the 8-byte records: 16 lanes per
 // bank); one pad slot per 16 records (per 8 BGR words) makes that stride odd in words.
-constexpr int kItemSlots = kTilePx + kTilePx / 16, kBgrSlots = kTilePx + kTilePx / 8;
-__device__ inline int item_slot(int m) { return m + (m >> 4); }
-__device__ inline int bgr_slot(int m) { return m + (m >> 3); }
+#ifndef SLG_ITEM_PAD
+#define SLG_ITEM_PAD 4                     // one pad record per 2^SLG_ITEM_PAD items
+#endif
+#ifndef SLG_BGR_PAD
+#define SLG_BGR_PAD 3                      // one pad word per 2^SLG_BGR_PAD BGR words
+#endif
+constexpr int kItemSlots = kTilePx + (kTilePx >> SLG_ITEM_PAD), kBgrSlots = kTilePx + (kTilePx >> SLG_BGR_PAD);
+__device__ inline int item_slot(int m) { return m + (m >> SLG_ITEM_PAD); }
+__device__ inline int bgr_slot(int m) { return m + (m >> SLG_BGR_PAD); }
 
 // Phase B of main3 for rounds [i, i + G) (item m = tid + 256 * round), FAST path: the G items'
 // loads and fp64 chains are independent, so their plane gathers are in flight together.
