@@ -143,6 +143,53 @@ def load_traffic_per_view():
 RESULT_OUT = sys.stdout          # main() points it at the original stdout
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_mode(gpus: int, env) -> str:
+    """How this invocation runs (decided before any GPU call):
+    ``"spawn"`` -- ``--gpus N > 1`` and no launcher: start N rank processes here;
+    ``"rank"``  -- a launcher (torchrun) set WORLD_SIZE and it equals ``--gpus``;
+    ``"single"`` -- one process, N = 1.
+    A WORLD_SIZE that disagrees with ``--gpus`` raises SystemExit (non-zero): a silent
+    one-rank measurement labelled N GPUs is never produced."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {gpus})")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise SystemExit(f"WORLD_SIZE={ws} disagrees with --gpus {gpus}")
+        return "rank" if gpus > 1 else "single"
+    return "spawn" if gpus > 1 else "single"
+
+
+def spawn_ranks(n: int, argv, script: str | None = None) -> int:
+    """Run ``bench.py`` as ``n`` rank processes on this node (one per GPU, LOCAL_RANK = RANK),
+    rendezvous on 127.0.0.1.  The parent never touches the GPU; rank 0's stdout (the JSON line)
+    is this process's stdout, the other ranks' stdout goes to stderr.  Returns the first
+    non-zero exit code, or 0."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__), *argv], env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    for p in procs:
+        code = p.wait()
+        if code and not rc:
+            rc = code
+            for q in procs:              # one rank failed: the others would wait at a barrier
+                if q.poll() is None:
+                    q.terminate()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -166,6 +213,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     args = ap.parse_args()
+    mode = launch_mode(args.gpus, os.environ)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     # stdout carries exactly ONE line, the JSON result: runtime banners that native libraries
     # print to fd 1 (RCCL's version block, gloo's peer lines) go to stderr with the logs
     global RESULT_OUT

@@ -44,10 +44,19 @@ def main(args, wl):
     if world == 1 and not args.no_cpu_baseline:
         cpu = bench.cpu_baseline([views[i] for i in range(lo, hi)], cal, args.cpu_seconds, wl)
 
+    # the one-GPU rehearsal knobs of bench.py (never set by the driver): every rank on one
+    # device, gloo instead of RCCL -- the gather then goes through host memory (two RCCL ranks
+    # cannot share a GPU)
+    if os.environ.get("SLG_BENCH_DEVICE"):
+        local = int(os.environ["SLG_BENCH_DEVICE"])
+    backend = os.environ.get("SLG_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     from structured_light_for_3d_model_replication_amd import engine as E
 
     cfg = E.DecodeConfig(PW, PH, NC, NR, "otsu")
@@ -62,7 +71,20 @@ def main(args, wl):
     preps = [beng.prepare([dframes[k] for k in g], cfg, dcal, [clouds[k] for k in g], row_mode, tol, slot=j)
              for j, g in enumerate(groups)]
     s = torch.cuda.Stream(device=dev)
-    gather = D.RcclCloudGather(device=dev)
+    gather = D.RcclCloudGather(device=dev) if backend == "nccl" else None
+    sizes = [D.shard_range(V, r, world) for r in range(world)]
+
+    def host_gather(parts):
+        """Rehearsal gather (gloo): per view slot, host copies through gather_clouds."""
+        by_rank = [[] for _ in range(world)]
+        for k in range(n_per_rank):
+            x, b = parts[k] if k < len(parts) else (clouds[0].xyz[:0], clouds[0].bgr[:0])
+            res = D.gather_clouds(x.cpu(), b.cpu(), dst=0)
+            if res is not None:
+                for r, (rx_, rb_) in enumerate(res):
+                    if k < sizes[r][1] - sizes[r][0]:
+                        by_rank[r].append((rx_, rb_))
+        return [c for r in by_rank for c in r] if rank == 0 else None
     host_x = host_b = None
     own_x = own_b = None
 
@@ -76,6 +98,8 @@ def main(args, wl):
         for c in clouds:
             n = int(c.count.item())
             parts.append((c.xyz[:n], c.bgr[:n]))
+        if gather is None:
+            return host_gather(parts)
         got = gather.gather(parts, n_per_rank, root=0, stream=s)
         if rank == 0:
             rx, rb = gather.last_buffers
@@ -193,7 +217,9 @@ def main(args, wl):
                                             "value": round(all_pts / (dt_alt / K) / 1e6, 2),
                                             "what": "each rank copies its own clouds to its own pinned host "
                                                     "memory, no collective"},
-                       "batch_views": B, "parallelism": f"view-sharded x{world} + RCCL gatherv"},
+                       "batch_views": B,
+                       "parallelism": f"view-sharded x{world} + " + ("RCCL gatherv (C ABI)" if gather is not None
+                                                                    else f"{backend} host gather (rehearsal)")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": bench.HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / bench.HBM_PEAK_GBS, 4) if achieved else None, "traffic": None,
@@ -202,6 +228,7 @@ def main(args, wl):
             "verify": verify,
         }
         print(json.dumps(out), file=getattr(args, "result_out", None) or sys.stdout, flush=True)
-    gather.close()
+    if gather is not None:
+        gather.close()
     if world > 1:
         dist.destroy_process_group()

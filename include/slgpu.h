@@ -216,7 +216,10 @@ int32_t slg_decode_stats_partials_batch(int32_t n_views, int32_t height, int32_t
  * thresholds by finishing workgroups at the front of this launch's grid -- the work of
  * slg_decode_stats_partials_batch without its kernel or a second stream.  Batch k's launch
  * carries batch k+2 and finishes batch k+1; fin_workspace must not be this launch's own
- * workspace.  Results are identical to slg_decode_stats_batch. */
+ * workspace.  The finished batch must share this launch's geometry (height, width) and decode
+ * parameters `dp` (its slices are read with them; nothing else identifies it).  ws_stride must
+ * be >= slg_workspace_bytes and 256-aligned whenever n_views, n_next or n_fin exceeds 1.
+ * Results are identical to slg_decode_stats_batch. */
 int32_t slg_decode_triangulate_batch_carry(const slg_capture *caps, int32_t n_views,
                                            const slg_decode_params *dp, const slg_calib *calib,
                                            const slg_tri_params *tp, void *workspace, int64_t ws_stride,
@@ -284,6 +287,15 @@ int32_t slg_gather_counts(slg_gather_comm *comm, const int64_t *counts, int32_t 
 int32_t slg_gatherv(slg_gather_comm *comm, const void *send, int64_t send_bytes, void *recv,
                     const int64_t *recv_bytes, int32_t root, void *stream);
 int32_t slg_gather_destroy(slg_gather_comm *comm);
+/* Host only, no RCCL: the plan slg_gatherv follows.  On the root (rank == root): checks
+ * recv_bytes (non-negative, recv_bytes[root] == send_bytes), writes offsets[n_ranks + 1] (rank
+ * r lands at recv + offsets[r], offsets[n_ranks] = total) and recv_from[n_ranks] (1 = a
+ * point-to-point receive from that peer; 0 for the root, whose own part is a device copy, and
+ * for zero-byte peers).  On other ranks: recv_from[0] = 1 when the rank sends (send_bytes > 0),
+ * offsets untouched.  Returns the number of point-to-point operations this rank issues, or a
+ * negative SLG_ERR_* code (slg_last_error() says why). */
+int32_t slg_gatherv_plan(int32_t n_ranks, int32_t rank, int32_t root, int64_t send_bytes,
+                         const int64_t *recv_bytes, int64_t *offsets, int32_t *recv_from);
 
 #ifdef __cplusplus
 }

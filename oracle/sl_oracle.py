@@ -197,7 +197,10 @@ def _intersect(planes, idx_map, valid, rays, Oc):
     p = planes[np.clip(idx_map.ravel()[valid], 0, planes.shape[0] - 1)]
     n0, n1, n2, d = p[:, 0], p[:, 1], p[:, 2], p[:, 3]
     denom = (n0 * rays[0] + n1 * rays[1]) + n2 * rays[2]
-    numer = ((n0 * Oc[0] + n1 * Oc[1]) + n2 * Oc[2]) + d     # == d for Oc = 0 (the calib value)
+    # processing.py:166,219: np.dot(N.T, Oc) -- the host BLAS's gemv rounding (e.g. OpenBLAS
+    # 0.3.29 here evaluates fma(n2,o2, fma(n0,o0, n1*o1))), reproduced by making the same call;
+    # == d for Oc = 0 (the calib value)
+    numer = np.dot(p[:, 0:3], Oc.reshape(3, 1)).flatten() + d
     ok = np.abs(denom) > 1e-6
     t = np.zeros_like(denom)
     t[ok] = -numer[ok] / denom[ok]

@@ -110,6 +110,8 @@ EXPORTS = {
     "slg_gather_counts": (c_i32, [c_vp, c_vp, c_i32, c_vp, c_vp]),
     "slg_gatherv": (c_i32, [c_vp, c_vp, c_i64, c_vp, ctypes.POINTER(c_i64), c_i32, c_vp]),
     "slg_gather_destroy": (c_i32, [c_vp]),
+    "slg_gatherv_plan": (c_i32, [c_i32, c_i32, c_i32, c_i64, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
+                                 ctypes.POINTER(c_i32)]),
 }
 GATHER_ID_BYTES = 128
 

@@ -25,7 +25,8 @@ def main(argv=None):
     ap.add_argument("--thresh", choices=["otsu", "manual"], default="otsu")
     ap.add_argument("--shadow-val", type=float, default=40)
     ap.add_argument("--contrast-val", type=float, default=10)
-    ap.add_argument("--batch-views", type=int, default=1, help="views per batched GPU launch (1..16)")
+    ap.add_argument("--batch-views", type=int, default=None,
+                    help="views per batched GPU launch (1..16; default: $SLG_BATCH_VIEWS, else 1)")
     a = ap.parse_args(argv)
 
     import torch
@@ -43,7 +44,7 @@ def main(argv=None):
                                 thresh_mode=a.thresh,
                                 shadow_val=int(a.shadow_val) if a.shadow_val.is_integer() else a.shadow_val,
                                 contrast_val=int(a.contrast_val) if a.contrast_val.is_integer() else a.contrast_val,
-                                batch_views=a.batch_views)
+                                **({} if a.batch_views is None else {"batch_views": a.batch_views}))
     finally:
         if world > 1:
             dist.destroy_process_group()

@@ -112,37 +112,56 @@ int32_t slg_gather_counts(slg_gather_comm* g, const int64_t* counts, int32_t n_p
   return SLG_OK;
 }
 
+int32_t slg_gatherv_plan(int32_t n_ranks, int32_t rank, int32_t root, int64_t send_bytes, const int64_t* recv_bytes,
+                         int64_t* offsets, int32_t* recv_from) {
+  if (n_ranks < 1 || rank < 0 || rank >= n_ranks || root < 0 || root >= n_ranks || send_bytes < 0 || !recv_from)
+    return -slg_internal_fail(SLG_ERR_INVALID, "bad gatherv argument");
+  if (rank != root) {
+    recv_from[0] = send_bytes > 0;
+    return send_bytes > 0;                     // the root skips zero-byte peers too
+  }
+  if (!recv_bytes || !offsets) return -slg_internal_fail(SLG_ERR_INVALID, "root needs recv_bytes, offsets");
+  if (recv_bytes[root] != send_bytes) return -slg_internal_fail(SLG_ERR_INVALID, "recv_bytes[root] != send_bytes");
+  int32_t ops = 0;
+  offsets[0] = 0;
+  for (int32_t r = 0; r < n_ranks; ++r) {
+    if (recv_bytes[r] < 0) return -slg_internal_fail(SLG_ERR_INVALID, "negative recv_bytes");
+    offsets[r + 1] = offsets[r] + recv_bytes[r];
+    recv_from[r] = (r != root && recv_bytes[r] > 0);
+    ops += recv_from[r];
+  }
+  return ops;
+}
+
 int32_t slg_gatherv(slg_gather_comm* g, const void* send, int64_t send_bytes, void* recv, const int64_t* recv_bytes,
                     int32_t root, void* stream) {
-  if (!g || send_bytes < 0 || root < 0 || root >= g->n_ranks || (send_bytes > 0 && !send))
-    return slg_internal_fail(SLG_ERR_INVALID, "bad gatherv argument");
+  if (!g || (send_bytes > 0 && !send)) return slg_internal_fail(SLG_ERR_INVALID, "bad gatherv argument");
+  std::vector<int64_t> off(size_t(g->n_ranks) + 1, 0);
+  std::vector<int32_t> from(size_t(g->n_ranks), 0);
+  const int32_t ops = slg_gatherv_plan(g->n_ranks, g->rank, root, send_bytes, recv_bytes, off.data(), from.data());
+  if (ops < 0) return -ops;
   RcclApi* a = rccl();
+  if (!a) return slg_internal_fail(SLG_ERR_UNSUPPORTED, "RCCL (librccl.so.1) not found");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (g->rank == root) {
-    if (!recv_bytes || (!recv && g->n_ranks > 0)) return slg_internal_fail(SLG_ERR_INVALID, "root needs recv, recv_bytes");
-    if (recv_bytes[root] != send_bytes) return slg_internal_fail(SLG_ERR_INVALID, "recv_bytes[root] != send_bytes");
-    std::vector<int64_t> off(size_t(g->n_ranks) + 1, 0);
-    for (int r = 0; r < g->n_ranks; ++r) {
-      if (recv_bytes[r] < 0) return slg_internal_fail(SLG_ERR_INVALID, "negative recv_bytes");
-      off[size_t(r) + 1] = off[size_t(r)] + recv_bytes[r];
-    }
-    char* dst = static_cast<char*>(recv);
-    if (send_bytes > 0 && hipMemcpyAsync(dst + off[size_t(root)], send, size_t(send_bytes), hipMemcpyDeviceToDevice, s) != hipSuccess)
-      return slg_internal_fail(SLG_ERR_HIP, "hipMemcpyAsync (root's own part) failed");
-    ncclResult_t r = a->group_start();
-    if (r != ncclSuccess) return nccl_fail(a, r, "ncclGroupStart");
-    for (int p = 0; p < g->n_ranks; ++p) {
-      if (p == root || recv_bytes[p] == 0) continue;
-      r = a->recv(dst + off[size_t(p)], size_t(recv_bytes[p]), ncclUint8, p, g->comm, s);
-      if (r != ncclSuccess) { a->group_end(); return nccl_fail(a, r, "ncclRecv"); }
-    }
-    r = a->group_end();
-    if (r != ncclSuccess) return nccl_fail(a, r, "ncclGroupEnd");
-    return SLG_OK;
+  if (g->rank != root) {
+    if (!ops) return SLG_OK;
+    const ncclResult_t r = a->send(send, size_t(send_bytes), ncclUint8, root, g->comm, s);
+    return r == ncclSuccess ? SLG_OK : nccl_fail(a, r, "ncclSend");
   }
-  if (send_bytes == 0) return SLG_OK;          // the root skips zero-byte peers too
-  const ncclResult_t r = a->send(send, size_t(send_bytes), ncclUint8, root, g->comm, s);
-  if (r != ncclSuccess) return nccl_fail(a, r, "ncclSend");
+  if (off[size_t(g->n_ranks)] > 0 && !recv) return slg_internal_fail(SLG_ERR_INVALID, "root needs recv");
+  char* dst = static_cast<char*>(recv);
+  if (send_bytes > 0 && hipMemcpyAsync(dst + off[size_t(root)], send, size_t(send_bytes), hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return slg_internal_fail(SLG_ERR_HIP, "hipMemcpyAsync (root's own part) failed");
+  if (!ops) return SLG_OK;
+  ncclResult_t r = a->group_start();
+  if (r != ncclSuccess) return nccl_fail(a, r, "ncclGroupStart");
+  for (int p = 0; p < g->n_ranks; ++p) {
+    if (!from[size_t(p)]) continue;
+    r = a->recv(dst + off[size_t(p)], size_t(recv_bytes[p]), ncclUint8, p, g->comm, s);
+    if (r != ncclSuccess) { a->group_end(); return nccl_fail(a, r, "ncclRecv"); }
+  }
+  r = a->group_end();
+  if (r != ncclSuccess) return nccl_fail(a, r, "ncclGroupEnd");
   return SLG_OK;
 }
 

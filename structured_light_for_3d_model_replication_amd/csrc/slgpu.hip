@@ -2153,7 +2153,10 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
     if (rc) return rc;
   }
   const int64_t n_px = int64_t(caps[0].height) * caps[0].width;
-  if (n_views > 1 && (ws_stride < ws_total(n_px) || (ws_stride & 255)))
+  // every slice of this launch (its views, the carried next batch, the finished batch) is
+  // ws_stride apart; the finished batch's slices are read with THIS batch's geometry and
+  // decode parameters (include/slgpu.h, slg_decode_triangulate_batch_carry)
+  if ((n_views > 1 || n_next > 1 || n_fin > 1) && (ws_stride < ws_total(n_px) || (ws_stride & 255)))
     return fail(SLG_ERR_INVALID, "ws_stride too small or not 256-aligned");
   Main3Params mp{};
   rc = fill_calib(mp.c, calib, tp, n_px, caps[0].width);
@@ -2517,7 +2520,6 @@ int32_t slg_decode_triangulate_batch_carry(const slg_capture* caps, int32_t n_vi
                                            int64_t ws_stride, const slg_cloud* outs, const slg_capture* next,
                                            int32_t n_next, void* fin_workspace, int32_t n_fin,
                                            void* const* timing_events, void* stream) {
-  if (n_fin > 1 && (ws_stride & 255)) return fail(SLG_ERR_INVALID, "ws_stride not 256-aligned");
   return fused_batch(caps, n_views, dp, calib, tp, static_cast<char*>(workspace), ws_stride, outs, timing_events,
                      static_cast<hipStream_t>(stream), next, next ? n_next : 0, static_cast<char*>(fin_workspace),
                      fin_workspace ? n_fin : 0);

@@ -100,6 +100,22 @@ def gather_clouds(xyz: torch.Tensor, bgr: torch.Tensor, dst: int = 0):
     return out
 
 
+def gather_plan(table, n_per_rank: int, xyz_dtype=None):
+    """The root's view of a gather from the all-gathered count table (host logic of
+    :meth:`RcclCloudGather.gather`, testable without RCCL).  ``table[r]`` is rank r's
+    ``n_per_rank`` view counts (-1 = padding slot) followed by its XYZ element width in bytes (0
+    when it holds no views).  Returns ``(xyz dtype, counts)`` with ``counts[r]`` the real views'
+    point counts of rank r; raises ``ValueError`` when ranks disagree on the width."""
+    seen = {int(row[n_per_rank]) for row in table} - {0}
+    if xyz_dtype is not None:
+        seen.add(torch.empty(0, dtype=xyz_dtype).element_size())
+    if len(seen) > 1:
+        raise ValueError(f"ranks hold XYZ clouds of different widths {sorted(seen)} bytes")
+    if xyz_dtype is None:
+        xyz_dtype = {4: torch.float32, 8: torch.float64}[seen.pop()] if seen else torch.float32
+    return xyz_dtype, [[int(c) for c in row[:n_per_rank] if c >= 0] for row in table]
+
+
 class RcclCloudGather:
     """The final cloud gather through the C ABI (``slg_gather_*`` over the process's RCCL):
     one communicator per job (its 128-byte id travels by a torch.distributed broadcast), then
@@ -134,41 +150,52 @@ class RcclCloudGather:
             self.N.check(self.N.lib().slg_gather_destroy(self.comm))
             self.comm = self.ct.c_void_p()
 
-    def gather(self, clouds, n_per_rank: int, root: int = 0, stream=None):
+    def gather(self, clouds, n_per_rank: int, root: int = 0, stream=None, xyz_dtype=None):
         """``clouds``: this rank's ``[(xyz [n,3], bgr [n,3] uint8), ...]`` (device tensors, at most
-        ``n_per_rank`` views).  Returns on ``root`` the list over every rank's views (rank-major)
-        of ``(xyz, bgr)`` slices of one gathered device buffer; ``None`` elsewhere."""
+        ``n_per_rank`` views; a rank may hold none).  Returns on ``root`` the list over every
+        rank's real views, rank-major (padding slots of ranks with fewer views are dropped), of
+        ``(xyz, bgr)`` slices of one gathered device buffer; ``None`` elsewhere.
+
+        The XYZ dtype is agreed across ranks, not guessed from a possibly empty list: every rank
+        sends its element width with its counts (0 when it holds no views), ``xyz_dtype``
+        (optional) fixes it, and ranks holding clouds of different widths raise ``ValueError``
+        on every rank before any byte moves."""
         N, ct = self.N, self.ct
         if len(clouds) > n_per_rank:
             raise ValueError("more views than n_per_rank")
+        widths = {x.element_size() for x, _ in clouds}
+        if len(widths) > 1 or (xyz_dtype is not None and clouds and clouds[0][0].dtype != xyz_dtype):
+            raise ValueError("this rank's clouds mix XYZ dtypes (or differ from xyz_dtype)")
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         sp = ct.c_void_p(s.cuda_stream)
-        dt = clouds[0][0].dtype if clouds else torch.float32
+        slots = n_per_rank + 1                    # per rank: view counts (-1 = padding), XYZ width
         with torch.cuda.stream(s):
-            cnt = torch.zeros(n_per_rank, dtype=torch.int64, device=self.device)
+            cnt = torch.full((slots,), -1, dtype=torch.int64, device=self.device)
             for k, (x, _) in enumerate(clouds):
                 cnt[k] = x.shape[0]
-            allc = torch.empty(self.world * n_per_rank, dtype=torch.int64, device=self.device)
-            N.check(N.lib().slg_gather_counts(self.comm, ct.c_void_p(cnt.data_ptr()), n_per_rank,
+            cnt[n_per_rank] = clouds[0][0].element_size() if clouds else 0
+            allc = torch.empty(self.world * slots, dtype=torch.int64, device=self.device)
+            N.check(N.lib().slg_gather_counts(self.comm, ct.c_void_p(cnt.data_ptr()), slots,
                                               ct.c_void_p(allc.data_ptr()), sp))
-            counts = allc.cpu().tolist()                  # sizes the root's buffers (host sync)
+            table = allc.cpu().view(self.world, slots).tolist()   # sizes the root's buffers (host sync)
+            dt, counts = gather_plan(table, n_per_rank, xyz_dtype)
+            esz = 3 * torch.empty(0, dtype=dt).element_size()
             xs = torch.cat([x.reshape(-1, 3) for x, _ in clouds]) if clouds else torch.empty((0, 3), dtype=dt, device=self.device)
             bs = torch.cat([b.reshape(-1, 3) for _, b in clouds]) if clouds else torch.empty((0, 3), dtype=torch.uint8, device=self.device)
-            per_rank = [sum(counts[r * n_per_rank:(r + 1) * n_per_rank]) for r in range(self.world)]
+            per_rank = [sum(c) for c in counts]
             total = sum(per_rank)
-            esz = xs.element_size() * 3
             rx = torch.empty((total, 3), dtype=dt, device=self.device) if self.rank == root else None
             rb = torch.empty((total, 3), dtype=torch.uint8, device=self.device) if self.rank == root else None
-            for send, recv, width in ((xs, rx, esz), (bs, rb, 3)):
-                rbytes = (ct.c_int64 * self.world)(*[c * width for c in per_rank])
-                N.check(N.lib().slg_gatherv(self.comm, ct.c_void_p(send.data_ptr()), send.shape[0] * width,
+            for send, recv, w in ((xs, rx, esz), (bs, rb, 3)):
+                rbytes = (ct.c_int64 * self.world)(*[c * w for c in per_rank])
+                N.check(N.lib().slg_gatherv(self.comm, ct.c_void_p(send.data_ptr()), send.shape[0] * w,
                                             ct.c_void_p(recv.data_ptr() if recv is not None else 0),
                                             rbytes, root, sp))
         self.last_buffers = (rx, rb)                      # root: the gathered job, contiguous
         if self.rank != root:
             return None
         out, off = [], 0
-        for c in counts:
+        for c in (c for row in counts for c in row):
             out.append((rx[off:off + c], rb[off:off + c]))
             off += c
         return out

@@ -25,8 +25,10 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
+
 
 import numpy as np
 import torch
@@ -41,16 +43,19 @@ class PinnedPool:
 
     def __init__(self):
         self._free: dict[int, list] = {}
+        self._lock = threading.Lock()       # get() on the reader threads, put() on the main one
 
     def get(self, nbytes: int) -> torch.Tensor:
-        lst = self._free.get(nbytes)
-        if lst:
-            return lst.pop()
+        with self._lock:
+            lst = self._free.get(nbytes)
+            if lst:
+                return lst.pop()
         return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
 
     def put(self, t: torch.Tensor | None):
         if t is not None:
-            self._free.setdefault(t.numel(), []).append(t)
+            with self._lock:
+                self._free.setdefault(t.numel(), []).append(t)
 
 
 @dataclass

@@ -31,37 +31,73 @@ def _engine(h, w):
     return _ENGINES[key]
 
 
-def calib_fingerprint(calib) -> str:
-    """Content digest of the calibration arrays the path reads (xxh3 over shapes, dtypes and
-    bytes): a cache keyed on it never serves tables of an edited or different calibration."""
+def _hasher():
     try:
         import xxhash
-        h = xxhash.xxh3_64()
+        return xxhash.xxh3_64()
     except ImportError:                     # pragma: no cover - xxhash ships with the image
         import hashlib
-        h = hashlib.blake2b(digest_size=16)
+        return hashlib.blake2b(digest_size=16)
+
+
+_NC_SAMPLE = 1 << 16                        # Nc elements hashed by the cheap fingerprint
+
+
+def calib_fingerprint(calib, full: bool = False) -> str:
+    """Digest of the calibration arrays the path reads (xxh3 over shapes, dtypes and bytes).
+
+    ``cam_K``, ``Oc`` and the plane tables (<= 131 KB) are always hashed whole.  ``Nc`` (3 x H*W
+    float64: 50 MB at 1080p, 576 MB at 24 MP) is hashed whole only with ``full=True``; the cheap
+    form hashes its shape, dtype and a strided sample of 65536 elements (first and last
+    included), which costs well under a millisecond at any size."""
+    h = _hasher()
     for k in ("cam_K", "Oc", "wPlaneCol", "wPlaneRow", "Nc"):
         a = calib.get(k) if hasattr(calib, "get") else None
         if a is None:
             h.update(f"{k}:none;".encode())
             continue
-        a = np.ascontiguousarray(a)
+        a = np.asarray(a)
         h.update(f"{k}:{a.shape}:{a.dtype.str};".encode())
-        h.update(memoryview(a).cast("B"))
+        if k == "Nc" and not full and a.size > _NC_SAMPLE:
+            flat = a.reshape(-1)            # a view for the contiguous table loadmat returns
+            a = flat[np.linspace(0, flat.size - 1, _NC_SAMPLE).astype(np.int64)]
+        h.update(memoryview(np.ascontiguousarray(a)).cast("B"))
     return h.hexdigest()
+
+
+def _ref(obj):
+    import weakref
+    try:
+        return weakref.ref(obj)
+    except TypeError:
+        return None
 
 
 def _device_calib(calib, h, w):
     """Device tables of ``calib`` for one geometry on the current GPU: a small LRU keyed on
-    (device, geometry, content digest), so it neither pins callers' dicts nor grows without
-    bound, and an edited calibration is uploaded afresh."""
+    (device, geometry, cheap content digest), so it neither pins callers' dicts nor grows
+    without bound, and an edited calibration is uploaded afresh.
+
+    A hit with the very ``Nc`` object of the cached entry costs only the cheap digest.  A hit
+    with another ``Nc`` object (e.g. the same ``.mat`` loaded again) is confirmed by the full
+    digest of its ``Nc`` against the one taken when the entry was made; a mismatch replaces the
+    entry.  (An in-place edit of ``Nc`` entries outside the sample, on the same object, is not
+    seen: edit a copy.)"""
     key = (torch.cuda.current_device(), h, w, calib_fingerprint(calib))
-    dc = _CALIBS.get(key)
-    if dc is not None:
-        _CALIBS.move_to_end(key)
-        return dc
+    nc = calib.get("Nc") if hasattr(calib, "get") else None
+    ent = _CALIBS.get(key)
+    if ent is not None:
+        dc, ref, full = ent
+        if nc is not None and ref is not None and ref() is nc:
+            _CALIBS.move_to_end(key)
+            return dc
+        if calib_fingerprint(calib, full=True) == full:
+            _CALIBS[key] = (dc, _ref(nc), full)
+            _CALIBS.move_to_end(key)
+            return dc
     dc = E.DeviceCalib(calib, h, w)
-    _CALIBS[key] = dc
+    _CALIBS[key] = (dc, _ref(nc), calib_fingerprint(calib, full=True))
+    _CALIBS.move_to_end(key)
     while len(_CALIBS) > _CALIBS_MAX:
         _CALIBS.popitem(last=False)
     return dc

@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import decode_kwargs, golden_cases, load_calibs, load_case
+from conftest import decode_kwargs, expected_cloud, golden_cases, load_calibs, load_case
 from oracle import sl_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -82,13 +82,15 @@ def test_cloud_bit_exact_f64(name, fused, mods):
                                   t(z["mask"], np.uint8), dev.texture, dc, row_mode=rm, xyz_f64=True)
         P, C = out.result()
         P, C = P.cpu().numpy(), C.cpu().numpy()
-        assert P.shape == z[f"P{rm}"].shape, (rm, P.shape, z[f"P{rm}"].shape)
-        assert np.array_equal(P, z[f"P{rm}"]), f"row_mode {rm}: max |d| {np.abs(P - z[f'P{rm}']).max()}"
-        assert np.array_equal(C, z[f"C{rm}"]), f"row_mode {rm} colours"
+        Pw, Cw = expected_cloud(z, cal, rm)
+        assert P.shape == Pw.shape, (rm, P.shape, Pw.shape)
+        assert np.array_equal(P, Pw), f"row_mode {rm}: max |d| {np.abs(P - Pw).max()}"
+        assert np.array_equal(C, Cw), f"row_mode {rm} colours"
         assert eng.error_flags() & 1 == 0
 
 
-@pytest.mark.parametrize("name", ["proc_otsu_full", "proc_c2style", "proc_odd_geometry", "sl_full"])
+@pytest.mark.parametrize("name", ["proc_otsu_full", "proc_c2style", "proc_odd_geometry", "sl_full",
+                                  "proc_oc_table", "proc_oc_krays", "proc_oc_raw"])
 def test_cloud_f32_within_tolerance(name, mods):
     E, PR, N = mods
     z = load_case(name)
