@@ -37,7 +37,6 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decoded+triangulated Mpoints/sec (1 GPU & 8-GPU node); % of HBM roofline"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.3 measured copy)
-CPU_SHARE = 16             # host CPUs per GPU on the GPU box (gpurun: size pools to 16)
 
 
 def log(*a):
@@ -95,13 +94,39 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(views, cal, seconds, wl):
-    """The oracle (NumPy restatement of the reference path, test infrastructure) on this host,
-    frames in memory: (i) one process, (ii) a process pool with one stream of views per worker
-    on the box's CPU share.  Runs BEFORE the GPU is touched (fork-safe).  `value` is the pool
-    figure, the stronger baseline."""
-    global _CPU_JOB
+def cpu_quota():
+    """CPUs of CPU time this process may use: the cgroup CFS quota (cgroup v2 ``cpu.max``, or v1
+    ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``), rounded up; None when unlimited.  On the GPU
+    box the affinity mask lists every host CPU (256) while the lease's quota is 16."""
+    import math
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, math.ceil(q / per))
+    except (OSError, ValueError):
+        return None
+
+
+def _pool_rate(workers, seconds):
     import multiprocessing as mp
+    with mp.get_context("fork").Pool(workers) as pool:
+        res = pool.map(_cpu_worker, [(seconds, w) for w in range(workers)])
+    return sum(r[0] for r in res), sum(r[1] for r in res), max(r[2] for r in res)
+
+
+def cpu_baseline(views, cal, seconds, wl):
+    """The oracle (NumPy restatement of the reference path, test infrastructure: in-memory
+    frames, prefix-XOR Gray decode, no imread) on this host: (i) one process, (ii) a process pool
+    with one stream of views per worker on every CPU the lease owns -- the affinity mask, capped
+    by the cgroup CPU quota when one is set (more processes than the quota only time-share it:
+    ``oversubscribed_2x`` measures that, with twice as many workers for half the time).  Runs
+    BEFORE the GPU is touched (fork-safe).  `value` is the pool figure, the stronger baseline."""
+    global _CPU_JOB
     import numpy as np
     _CPU_JOB = (views, cal, wl["proj"], wl["nsets"])
     nsets = wl["nsets"]
@@ -110,21 +135,25 @@ def cpu_baseline(views, cal, seconds, wl):
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    workers = max(1, min(avail, CPU_SHARE))
-    with mp.get_context("fork").Pool(workers) as pool:
-        res = pool.map(_cpu_worker, [(seconds, w) for w in range(workers)])
-    pts = sum(r[0] for r in res)
-    n_views = sum(r[1] for r in res)
-    wall = max(r[2] for r in res)
+    quota = cpu_quota()
+    workers = max(1, min(avail, quota or avail))
+    pts, n_views, wall = _pool_rate(workers, seconds)
+    over = None
+    if quota is not None and quota < avail:
+        p2, v2, w2 = _pool_rate(min(avail, 2 * workers), seconds / 2)
+        over = {"workers": min(avail, 2 * workers), "value": round(p2 / w2 / 1e6, 4), "views": v2,
+                "what": "2x the quota in worker processes, ~half the time: the quota, not the process "
+                        "count, bounds the host"}
     tag = wl["text"].split(":")[0]
     return {"value": round(pts / wall / 1e6, 4), "unit": "Mpoints/s", "cores": workers, "kind": "port",
             "sample": f"{n_views} {tag} views ({wl['cam'][0]}x{wl['cam'][1]}, {nsets[0]}+{nsets[1]} bits, Otsu, "
-                      f"row_mode 1) on {workers} worker processes x ~{seconds:.0f} s, frames in memory, "
-                      "oracle/sl_oracle.py NumPy restatement of server/processing.py:28-234",
+                      f"row_mode 1) on {workers} worker processes x ~{seconds:.0f} s, frames in memory",
+            "what": "oracle/sl_oracle.py: NumPy restatement of server/processing.py:28-234 (in-memory frames, "
+                    "prefix-XOR Gray decode, no imread), one view stream per process",
             "single_process_value": round(one[0] / one[2] / 1e6, 4),
             "single_process_sample": f"{one[1]} views in {one[2]:.1f} s, 1 process",
-            "host_cpus": os.cpu_count(), "cpus_available": avail, "cpu_model": _cpu_model(),
-            "numpy": np.__version__}
+            "host_cpus": os.cpu_count(), "cpus_available": avail, "cpu_quota": quota,
+            "oversubscribed_2x": over, "cpu_model": _cpu_model(), "numpy": np.__version__}
 
 
 def load_traffic_per_view():

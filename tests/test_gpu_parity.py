@@ -510,3 +510,26 @@ def test_partial_histograms_match_frame_stats(mods, hw):
     torch.cuda.synchronize()
     for o, o1 in zip(outs, outs1):
         assert torch.equal(o.result()[0], o1.result()[0])
+
+
+@pytest.mark.parametrize("name,shape", [("single_bin_0", (25, 40)), ("single_bin_255", (25, 40)),
+                                        ("exact_tie_scaled", (27, 37))])
+def test_otsu_edge_and_tie_thresholds(name, shape, mods):
+    """The GPU Otsu (stats pass) on the KAT histograms of tests/test_oracle_kat.py: a single
+    non-empty bin at 0 / 255, and an exact sigma tie between two splits that sequential fp64
+    resolves to the second (OpenCV's C getThreshVal_Otsu_8u order)."""
+    E, PR, N = mods
+    import torch
+    from test_oracle_kat import OTSU_CASES
+    h, want, _ = OTSU_CASES[name]
+    vals = np.repeat(np.arange(256), h).astype(np.uint8)
+    assert vals.size == shape[0] * shape[1]
+    white = np.random.default_rng(5).permutation(vals).reshape(shape)
+    black = np.zeros(shape, np.uint8)
+    frames = torch.from_numpy(np.stack([white, black, white, black])).cuda()
+    dev = E.DeviceFrames(frames)
+    eng = E.Reconstructor(*shape)
+    eng.stats(dev, E.DecodeConfig(1920, 1080, 11, 11, "otsu"))
+    torch.cuda.synchronize()
+    ts, tc = eng.thresholds()
+    assert (ts, tc) == (want, want) == (O.otsu_threshold(white), O.otsu_threshold(white))

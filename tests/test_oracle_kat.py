@@ -125,3 +125,60 @@ def test_gray_code_round_trip(bits):
         p, i = col_frames[2 * b][0], col_frames[2 * b + 1][0]
         g |= (p > i).astype(np.int32) << (bits - 1 - b)
     assert np.array_equal(O._gray_to_binary(g), np.arange(n))
+
+
+# ---- Otsu cases where an OpenCV build other than the C path could diverge.
+# The restatement is OpenCV's C getThreshVal_Otsu_8u; opencv-python wheels may dispatch to
+# IPP's ippiComputeThreshold_Otsu, whose agreement is unpinned here.  These fix what the C
+# recurrence returns (the GPU's otsu_wave / otsu_from_parts follow it, tests/test_gpu_parity.py).
+def _hist(pairs):
+    h = [0] * 256
+    for v, c in pairs:
+        h[v] += c
+    return h
+
+
+def cross_tie(h):
+    """Exact-rational maxima of sigma at thresholds with DIFFERENT class splits (q1), i.e. a
+    real tie, not a plateau of empty bins (which the strict '>' resolves to its first bin)."""
+    n = sum(h)
+    mu = Fraction(sum(i * c for i, c in enumerate(h)), n)
+    mu1, q1, sig = Fraction(0), Fraction(0), []
+    for i in range(256):
+        p = Fraction(h[i], n)
+        mu1 *= q1
+        q1 += p
+        q2 = 1 - q1
+        if min(q1, q2) < EPS or max(q1, q2) > 1 - EPS:
+            continue
+        mu1 = (mu1 + i * p) / q1
+        mu2 = (mu - q1 * mu1) / q2
+        sig.append((q1 * q2 * (mu1 - mu2) ** 2, q1))
+    if not sig:
+        return False
+    best = max(s for s, _ in sig)
+    return len({q for s, q in sig if s == best}) > 1
+
+
+OTSU_CASES = {
+    # name: (histogram, value the C recurrence returns, exact-rational tie across splits?)
+    "single_bin_0": (_hist([(0, 1000)]), 0.0, False),        # every bin skipped (q1 or q2 ~ 0)
+    "single_bin_255": (_hist([(255, 1000)]), 0.0, False),
+    "single_bin_128": (_hist([(128, 7)]), 0.0, False),
+    "two_bins_0_255": (_hist([(0, 3), (255, 1)]), 0.0, False),   # plateau 0..254: first bin
+    "symmetric_4": (_hist([(10, 5), (20, 5), (30, 5), (40, 5)]), 20.0, False),
+    # {0, 100, 200} x 1: splitting after 0 or after 100 gives sigma = (2/9) * 150^2 exactly; in
+    # sequential fp64 the second split's sigma rounds higher, so the C path returns 100 where
+    # exact arithmetic (and any differently-ordered implementation) may return 0
+    "exact_tie_3bins": (_hist([(0, 1), (100, 1), (200, 1)]), 100.0, True),
+    "exact_tie_scaled": (_hist([(20, 333), (90, 333), (160, 333)]), 90.0, True),
+}
+
+
+@pytest.mark.parametrize("name", sorted(OTSU_CASES))
+def test_otsu_edge_and_tie_cases(name):
+    h, want, tie = OTSU_CASES[name]
+    assert O.otsu_from_hist(h) == want
+    assert cross_tie(h) == tie
+    if not tie:
+        assert float(otsu_exact(h)[0]) == want

@@ -101,7 +101,11 @@ def main():
     for r in range(a.rounds):
         for lib in libs:
             env = dict(os.environ)
-            path, _, opt = lib.partition(":")
+            spec, _, envs = lib.partition("@")          # lib[:tables][@NAME=VAL+NAME=VAL]
+            for kv in filter(None, envs.split("+")):
+                k, _, v = kv.partition("=")
+                env[k] = v
+            path, _, opt = spec.partition(":")
             if path:
                 env["SLG_LIB"] = path
             cmd = [sys.executable, __file__, "--worker", "--launches", str(a.launches), "--warmup", str(a.warmup)]

@@ -38,6 +38,9 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--kernel", default="main3_kernel")
     ap.add_argument("--tiles-per-view", type=int, default=507, help="ceil(1920*1080 / 4096)")
+    ap.add_argument("--timed-last", type=int, default=0,
+                    help="also report the mean over the last N launches of the most frequent grid (the "
+                         "bench's timed steps: the trace run's --steps; settle/warmup launches excluded)")
     ap.add_argument("--no-refresh", action="store_true",
                     help="leave profiles/pmc_main_kernel.json (bench.py's C2 traffic) untouched")
     a = ap.parse_args()
@@ -52,16 +55,28 @@ def main():
 
     # kernel trace: duration per launch grouped by grid size
     by_grid = collections.defaultdict(list)
+    timed = collections.defaultdict(list)           # grid -> [(start, duration us)] in launch order
     for r in rows_of(os.path.join(src, "trace", "trace_kernel_trace.csv"), a.kernel):
-        by_grid[int(r["Grid_Size_X"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        by_grid[int(r["Grid_Size_X"])].append(d)
+        timed[int(r["Grid_Size_X"])].append((int(r["Start_Timestamp"]), d))
     # a pipelined launch also carries its finishing workgroups (fewer than one view's tiles)
     vof = lambda g: max(1, g // grid_threads_per_view)
     trace = {str(g): {"views": vof(g), "launches": len(d),
                       "avg_us": round(statistics.mean(d), 2),
                       "avg_us_per_view": round(statistics.mean(d) / vof(g), 2)}
              for g, d in sorted(by_grid.items())}
+    res = {"kernel": a.kernel, "by_grid_threads": trace}
+    if a.timed_last and timed:
+        g = max(timed, key=lambda k: len(timed[k]))
+        last = [d for _, d in sorted(timed[g])][-a.timed_last:]
+        res["timed_steps"] = {"grid_threads": g, "views": vof(g), "launches": len(last),
+                              "avg_us": round(statistics.mean(last), 2),
+                              "median_us": round(statistics.median(last), 2),
+                              "what": f"the last {a.timed_last} launches of the most frequent grid, in start order "
+                                      "(the bench's timed steps; settle, cold-start and warmup launches excluded)"}
     with open(os.path.join(dst, "kernel_by_grid.json"), "w") as f:
-        json.dump({"kernel": a.kernel, "by_grid_threads": trace}, f, indent=1)
+        json.dump(res, f, indent=1)
 
     # PMC: HBM bytes per view
     out = {"source": f"gpurun_out/{a.tag}", "kernel": a.kernel,
@@ -84,7 +99,7 @@ def main():
             json.dump({"tag": a.tag, "kernel": a.kernel, "hbm_bytes_per_view": out["hbm_bytes_per_view"],
                        "fetch_bytes_per_view": out.get("fetch_size_bytes_per_view"),
                        "write_bytes_per_view": out.get("write_size_bytes_per_view")}, f, indent=1)
-    print(json.dumps({"trace": trace, "pmc": out}, indent=1))
+    print(json.dumps({"trace": res, "pmc": out}, indent=1))
 
 
 if __name__ == "__main__":
