@@ -230,10 +230,11 @@ def main():
     ap.add_argument("--copies", type=int, default=None, help="device copies of each view in the pool")
     ap.add_argument("--batch", type=int, default=None, help="views per fused launch (<= 16)")
     ap.add_argument("--xyz", choices=["f32", "f64"], default="f32")
-    ap.add_argument("--pipeline", choices=["serial", "overlap", "fused"], default="fused",
+    ap.add_argument("--pipeline", choices=["serial", "overlap", "fused", "fused2"], default="fused",
                     help="serial: stats + fused launch per batch on one stream; overlap: the next "
                          "batch's stats on a side stream during this batch's fused launch; fused: "
-                         "batch k's fused launch computes batch k+2's histograms")
+                         "batch k's fused launch computes batch k+2's histograms; fused2: the same on two "
+                         "streams (batch k on stream k %% 2, carrying batch k+4), launches overlap")
     ap.add_argument("--settle-ms", type=float, default=60.0,
                     help="untimed launches (ms of GPU time) before the warmup, for the clocks to ramp")
     ap.add_argument("--kernel-events", choices=["launch", "region"], default="region",
@@ -309,8 +310,9 @@ def main():
     B = max(1, min(args.batch, E.MAX_VIEWS_PER_LAUNCH, P))
     s_main = torch.cuda.Stream(device=dev)
     s_stats = torch.cuda.Stream(device=dev)
-    beng = E.BatchReconstructor(H, W, B, device=dev, slots=2)
-    clouds = [[E.Cloud(H * W, row_mode, f64, device=dev) for _ in range(B)] for _ in range(2)]
+    NSL = 4 if args.pipeline == "fused2" else 2      # workspace / cloud slots (batch k on slot k % NSL)
+    beng = E.BatchReconstructor(H, W, B, device=dev, slots=NSL)
+    clouds = [[E.Cloud(H * W, row_mode, f64, device=dev) for _ in range(B)] for _ in range(NSL)]
     preps = {}
 
     def prep(start, slot):
@@ -333,7 +335,7 @@ def main():
     K, Wm = args.steps, args.warmup
     # the whole run as ONE batch stream: warmup + timed + 2 look-ahead batches whose thresholds
     # the last timed launches prepare (carried histograms), as every other step does
-    batches = [prep(b * B, b % 2) for b in range(Wm + K + 2)]
+    batches = [prep(b * B, b % NSL) for b in range(Wm + K + NSL)]
     # HIP events on the launch stream: one pair per fused launch ("launch": kernel time alone),
     # or one pair around the timed region ("region": launches + the gaps between them)
     n_ev = K if args.kernel_events == "launch" else 1
@@ -352,7 +354,7 @@ def main():
     bytes_alg = sum(frame_b + out_b * pts[v] for b in range(Wm, Wm + K) for v in pool_views(b))
 
     def run_range(lo, hi, events=None):
-        if args.pipeline in ("overlap", "fused"):
+        if args.pipeline in ("overlap", "fused", "fused2"):
             beng.run_pipelined(batches, s_main, s_stats, events=events, mode=args.pipeline, start=lo, stop=hi)
         else:
             for k in range(lo, hi):
@@ -362,8 +364,8 @@ def main():
     # of GPU time before the pipeline starts (then the cold start, warmup and timed steps)
     settle = max(0, int(round(args.settle_ms / 0.35)))
     if settle:
-        sb = [prep(b * B, b % 2) for b in range(settle + 2)]
-        if args.pipeline in ("overlap", "fused"):
+        sb = [prep(b * B, b % NSL) for b in range(settle + NSL)]
+        if args.pipeline in ("overlap", "fused", "fused2"):
             beng.run_pipelined(sb, s_main, s_stats, mode=args.pipeline, start=0, stop=settle)
         else:
             for k in range(settle):
@@ -384,7 +386,11 @@ def main():
         run_range(Wm, Wm + K, events=[(a.cuda_event, b.cuda_event) for a, b in ev])
     else:
         ev[0][0].record(s_main)
+        if args.pipeline == "fused2":
+            s_stats.wait_event(ev[0][0])              # the second stream starts there too
         run_range(Wm, Wm + K)
+        if args.pipeline == "fused2":
+            s_main.wait_stream(s_stats)
         ev[0][1].record(s_main)
     t_enq = time.perf_counter() - t0              # host time to enqueue the K steps
     torch.cuda.synchronize()
@@ -394,14 +400,14 @@ def main():
     dt = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in ev)
     helper_runs = sum(int(np.frombuffer(beng.header(s, k)[3084:3088].cpu().numpy().tobytes(), np.uint32)[0] & 2 != 0)
-                      for s in range(2) for k in range(B))
+                      for s in range(NSL) for k in range(B))
 
     # ---- verification, outside the timed region: the last timed batch's clouds (nothing wrote
     # its slot after it) against the plain batch path (bitwise) and one view against the oracle
     verify = None
     if not args.no_verify:
         last = Wm + K - 1
-        slot = last % 2
+        slot = last % NSL
         got = [(int(c.count.item()), c.xyz[: int(c.count.item())].clone(), c.bgr[: int(c.count.item())].clone())
                for c in clouds[slot]]
         ref_b = prep(last * B, slot)

@@ -82,6 +82,37 @@ def stripe_planes(K2: np.ndarray, R: np.ndarray, T: np.ndarray,
     return col, row
 
 
+def stripe_planes_fast(K2: np.ndarray, R: np.ndarray, T: np.ndarray,
+                       proj_w: int, proj_h: int) -> tuple[np.ndarray, np.ndarray]:
+    """:func:`stripe_planes` as whole-array NumPy (opt-in, ~150x faster: 1.3 ms vs 0.19 s for a
+    1920x1080 projector).  NOT bit-identical to the reference: batched matmul / einsum round
+    differently from the per-plane BLAS gemv / ddot / nrm2 calls of ``get_plane_from_proj_line``
+    (``server/sl_system.py:386-410``) -- measured on the default rig: 566 of 1920 column planes
+    and 474 of 1080 row planes differ, by at most 4 ulps (6.4e-16 relative).  Which rounding the
+    reference itself gets depends on the host's BLAS kernel, so no fixed batched formula can
+    match it everywhere: :func:`stripe_planes` (the per-plane loop, once per rig) stays the
+    bit-exact path and the default of :func:`build_tables`."""
+    K2 = np.asarray(K2, dtype=np.float64)
+    fxp, fyp, cxp, cyp = K2[0, 0], K2[1, 1], K2[0, 2], K2[1, 2]
+    Rinv = np.asarray(R, dtype=np.float64).T
+    C = (-Rinv @ np.asarray(T, dtype=np.float64).reshape(3, 1)).flatten()
+
+    def planes(p1, p2):
+        n = np.cross(p1 @ Rinv.T, p2 @ Rinv.T)
+        n /= np.sqrt(np.einsum("ij,ij->i", n, n))[:, None]
+        return np.column_stack([n, -(n @ C)])
+
+    pw, ph = int(proj_w), int(proj_h)
+    x = (np.arange(pw) - cxp) / fxp
+    y = (np.arange(ph) - cyp) / fyp
+    one_w, one_h = np.ones(pw), np.ones(ph)
+    col = planes(np.column_stack([x, np.full(pw, (0 - cyp) / fyp), one_w]),
+                 np.column_stack([x, np.full(pw, (ph - cyp) / fyp), one_w]))
+    row = planes(np.column_stack([np.full(ph, (0 - cxp) / fxp), y, one_h]),
+                 np.column_stack([np.full(ph, (pw - cxp) / fxp), y, one_h]))
+    return col, row
+
+
 def build_tables(K1, K2, R, T, cam_size, proj_size, dist=None) -> dict:
     """All tables ``calibrate_final`` saves (``server/sl_system.py:413-423``), reference shapes.
 

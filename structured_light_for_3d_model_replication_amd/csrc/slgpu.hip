@@ -1268,6 +1268,10 @@ constexpr int kMaxViews = 16;
 #ifndef SLG_TRI_GROUP
 #define SLG_TRI_GROUP 4                    // phase B: rounds (items per lane) whose gathers are in flight together
 #endif
+#ifndef SLG_TEX_LATE
+#define SLG_TEX_LATE 1                     // texture bytes read only by lanes with a valid pixel, after the
+                                           // decode (285.1 vs 289.7 us per 12-view launch, profiles/r3d/ab.log)
+#endif
 #ifndef SLG_M3_WAVES
 #define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
 #endif
@@ -1550,18 +1554,24 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   int n_items;
   {
     uint32_t tex[6] = {0, 0, 0, 0, 0, 0};
-    if (!tail) {
-      const uint32_t tq = uint32_t(px0) * 3u;     // n_px * 3 < 2^32 (host: slg_capture checks)
-      const uint2 t0 = ld_once8_buf(p.texture, tq), t1 = ld_once8_buf(p.texture, tq + 8u),
-                  t2 = ld_once8_buf(p.texture, tq + 16u);
-      tex[0] = t0.x; tex[1] = t0.y; tex[2] = t1.x; tex[3] = t1.y; tex[4] = t2.x; tex[5] = t2.y;
-    } else {
-      for (int k = 0; k < 3 * kPx; ++k)
-        if (px0 * 3 + k < p.n_px * 3) tex[k >> 2] |= uint32_t(p.texture[px0 * 3 + k]) << (8 * (k & 3));
-    }
+    auto load_tex = [&]() {
+      if (!tail) {
+        const uint32_t tq = uint32_t(px0) * 3u;   // n_px * 3 < 2^32 (host: slg_capture checks)
+        const uint2 t0 = ld_once8_buf(p.texture, tq), t1 = ld_once8_buf(p.texture, tq + 8u),
+                    t2 = ld_once8_buf(p.texture, tq + 16u);
+        tex[0] = t0.x; tex[1] = t0.y; tex[2] = t1.x; tex[3] = t1.y; tex[4] = t2.x; tex[5] = t2.y;
+      } else {
+        for (int k = 0; k < 3 * kPx; ++k)
+          if (px0 * 3 + k < p.n_px * 3) tex[k >> 2] |= uint32_t(p.texture[px0 * 3 + k]) << (8 * (k & 3));
+      }
+    };
+    if (!SLG_TEX_LATE) load_tex();
     uint32_t valid;
     int col[kPx], row[kPx];
     decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH>(p, px0, tail, valid, col, row);
+    // SLG_TEX_LATE: only lanes with a valid pixel read their 24 texture bytes, once the mask is
+    // known (the block scan's barrier covers part of the latency)
+    if (SLG_TEX_LATE && valid != 0u) load_tex();
     const int2 sc = block_scan(__popc(valid), s_wtot);
     n_items = sc.y;
     int m = sc.x;
@@ -2067,6 +2077,10 @@ Main3Fn pick_main(int row_mode, int x64, int rays) {
   if (debug_flags() & kMainDbgBits)
     return (SRC == 1 && row_mode == 1 && x64 == 0 && rays == SLG_RAYS_PINHOLE) ? main3_kernel<1, 0, 1, 1, true> : nullptr;
 #define SLG_CASE(RM, X, R) if (row_mode == RM && x64 == X && rays == R) return main3_kernel<RM, X, SRC, R, false>;
+#ifdef SLG_FAST_BUILD   // register/spill inspection builds only: the benchmark's instance alone
+  SLG_CASE(1, 0, 1)
+  return nullptr;
+#endif
   SLG_CASE(0, 0, 0) SLG_CASE(0, 0, 1) SLG_CASE(0, 1, 0) SLG_CASE(0, 1, 1)
   SLG_CASE(1, 0, 0) SLG_CASE(1, 0, 1) SLG_CASE(1, 1, 0) SLG_CASE(1, 1, 1)
   SLG_CASE(2, 0, 0) SLG_CASE(2, 0, 1) SLG_CASE(2, 1, 0) SLG_CASE(2, 1, 1)

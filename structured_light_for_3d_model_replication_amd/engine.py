@@ -453,6 +453,39 @@ class BatchReconstructor:
         N.check(N.lib().slg_decode_stats_partials_batch(pb.n, self.height, self.width, ctypes.byref(pb.dp),
                                                         self._ws(pb.slot), self.ws_stride, _stream(stream)))
 
+    def _run_fused2(self, batches, s0, s1, ev_of, start, stop):
+        """mode "fused2": the fused pipeline on TWO streams, batch k on stream k % 2, so launch
+        k+1 fills the GPU while launch k's last workgroups drain (no launch boundary between
+        them).  Every dependency stays on one stream: launch k carries batch k+4's histograms
+        (same slot) and finishes batch k+2's thresholds (partials from launch k-2); batches
+        0..3 get a regular stats pass.  Needs 4 workspace slots, batch k on slot k % 4."""
+        n = len(batches)
+        if s1 is None:
+            raise ValueError("fused2 needs a second stream")
+        for k in range(n):
+            for d in (1, 2, 3):
+                if k + d < n and batches[k + d].slot == batches[k].slot:
+                    raise ValueError("fused2: batches k..k+3 need four different slots")
+            if k + 4 < n and batches[k + 4].slot != batches[k].slot:
+                raise ValueError("fused2: batch k+4 must reuse batch k's slot")
+        if not all(b.dp.thresh_mode == N.THRESH_OTSU for b in batches):
+            raise ValueError("fused2 needs Otsu thresholds")
+        streams = (s0, s1)
+
+        def carried(j):          # batch j's histograms ride on launch j-4
+            return (j >= 4 and batches[j].n <= batches[j - 4].n and batches[j].n <= MAX_VIEWS_PER_LAUNCH)
+
+        if start == 0:
+            for k in range(min(4, n)):
+                self.stats(batches[k], stream=streams[k % 2])
+        for k in range(start, stop):
+            s = streams[k % 2]
+            nxt = batches[k + 4] if k + 4 < n and carried(k + 4) else None
+            fin = batches[k + 2] if k + 2 < n and carried(k + 2) else None
+            self.main_carry(batches[k], nxt, fin, events=ev_of(k), stream=s)
+            if k + 4 < n and nxt is None:                  # not carried: a regular pass, after
+                self.stats(batches[k + 4], stream=s)       # batch k is done with the slot
+
     @staticmethod
     def _carried(batches, j) -> bool:
         """Whether batch j's histograms ride on batch j-2's fused launch (same slot, no more views)."""
@@ -489,6 +522,8 @@ class BatchReconstructor:
         def ev_of(k):
             return None if events is None else events[k - start]
 
+        if mode == "fused2":
+            return self._run_fused2(batches, main_stream, stats_stream, ev_of, start, stop)
         if mode == "fused" and n and all(b.dp.thresh_mode == N.THRESH_OTSU for b in batches):
             s = main_stream
             if start == 0:

@@ -93,6 +93,35 @@ def test_c2_bench_launch_shape(mods, scan):
     assert min(len(w[0]) for w in want) > 500_000
 
 
+def test_c2_two_stream_pipeline(mods, scan):
+    """bench.py --pipeline fused2: batch k on stream k % 2 (launches overlap), launch k carrying
+    batch k+4's histograms and finishing batch k+2's thresholds, 4 slots; 6-view batches over
+    the 36 views, issued in two pieces.  Every count against the oracle, clouds on a subset."""
+    E, N = mods
+    import torch
+    cal, views = scan
+    want = _oracle_all(cal, views, (11, 10))
+    dev = [E.DeviceFrames(list(v.frames), v.texture) for v in views]
+    dcal = E.DeviceCalib(cal, 1080, 1920)
+    cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
+    eng = E.BatchReconstructor(1080, 1920, 6, slots=4)
+    clouds = [E.Cloud(1920 * 1080, 1, False) for _ in range(N_VIEWS)]
+    batches = [eng.prepare(dev[6 * b:6 * b + 6], cfg, dcal, clouds[6 * b:6 * b + 6], 1, 2.0, slot=b % 4)
+               for b in range(6)]
+    s0, s1 = torch.cuda.Stream(), torch.cuda.Stream()
+    eng.run_pipelined(batches, s0, s1, mode="fused2", start=0, stop=2)
+    torch.cuda.synchronize()
+    eng.run_pipelined(batches, s0, s1, mode="fused2", start=2, stop=6)
+    torch.cuda.synchronize()
+    for k, (c, (Po, Co)) in enumerate(zip(clouds, want)):
+        P, C = c.result()
+        assert P.shape[0] == Po.shape[0], (k, P.shape[0], Po.shape[0])
+        if k % 5 == 0:
+            assert np.array_equal(C.cpu().numpy(), Co), k
+            _xyz32_close(P.cpu().numpy(), Po)
+    assert all(eng.header(s, v)[3084:3088].cpu().numpy()[0] & 1 == 0 for s in range(4) for v in range(6))
+
+
 def test_c3_sharded_job(mods, scan):
     """C3: 36 views, 11 + 11 bits, 12-view batches, then the C-ABI RCCL gatherv (world 1)."""
     E, N = mods

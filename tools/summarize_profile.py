@@ -59,7 +59,7 @@ def main():
     for r in rows_of(os.path.join(src, "trace", "trace_kernel_trace.csv"), a.kernel):
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         by_grid[int(r["Grid_Size_X"])].append(d)
-        timed[int(r["Grid_Size_X"])].append((int(r["Start_Timestamp"]), d))
+        timed[int(r["Grid_Size_X"])].append((int(r["Start_Timestamp"]), d, int(r["End_Timestamp"])))
     # a pipelined launch also carries its finishing workgroups (fewer than one view's tiles)
     vof = lambda g: max(1, g // grid_threads_per_view)
     trace = {str(g): {"views": vof(g), "launches": len(d),
@@ -69,10 +69,15 @@ def main():
     res = {"kernel": a.kernel, "by_grid_threads": trace}
     if a.timed_last and timed:
         g = max(timed, key=lambda k: len(timed[k]))
-        last = [d for _, d in sorted(timed[g])][-a.timed_last:]
+        rows = sorted(timed[g])[-a.timed_last:]
+        last = [d for _, d, _ in rows]
+        # launches on two streams (--pipeline fused2) overlap: a launch's own duration then
+        # exceeds the step; the span of the timed launches per launch is the step period
+        span = (max(e for _, _, e in rows) - rows[0][0]) / 1e3 / len(rows)
         res["timed_steps"] = {"grid_threads": g, "views": vof(g), "launches": len(last),
                               "avg_us": round(statistics.mean(last), 2),
                               "median_us": round(statistics.median(last), 2),
+                              "span_us_per_launch": round(span, 2),
                               "what": f"the last {a.timed_last} launches of the most frequent grid, in start order "
                                       "(the bench's timed steps; settle, cold-start and warmup launches excluded)"}
     with open(os.path.join(dst, "kernel_by_grid.json"), "w") as f:
