@@ -5,13 +5,18 @@ Workload (BASELINE.json configs[1], "C2"): 1920x1080 views, 11 column + 10 row G
 with inverses + white/black (44 frames), Otsu mask, row_mode 1 (epipolar filter, tol 2.0),
 fp32 XYZ + BGR out, inputs resident in HBM.  A STEP is one batch of B views (default 12) through
 the whole path: ONE fused decode/triangulate/compaction launch over the batch, plus its Otsu
-thresholds -- in the default ``--pipeline fused`` the launch of batch k also counts batch k+2's
-histograms (per-tile partials) and a small kernel on a side stream turns them into thresholds
-beside batch k+1's launch (BatchReconstructor.run_pipelined).  The pipeline runs continuously
-from the priming stats passes (outside any timing) through the W warmup steps into the K timed
-steps, so every timed step is a steady-state step whatever K is.  Steps rotate over a pool of
-distinct rendered turntable views (views x copies HBM buffers, > 256 MiB Infinity Cache), so
-frames stream from HBM and a carried batch is never the batch being decoded.
+thresholds.  Default ``--pipeline fused2``: batch k's launch runs on stream k % 2, counts batch
+k+4's histograms (per-tile partials: no separate pass over its white/black frames) and, with
+workgroups at the front of its grid, turns batch k+2's partials into thresholds; every
+dependency stays on one stream, so launch k+1 fills the GPU while launch k's last workgroups
+drain (BatchReconstructor.run_pipelined; ``fused`` is the same on one stream with distance 2).
+The pipeline runs continuously from the priming stats passes (outside any timing) through the
+W warmup steps into the K timed steps, so every timed step is a steady-state step whatever K
+is.  Steps rotate over a pool of distinct rendered turntable views (views x copies HBM buffers,
+> 256 MiB Infinity Cache), so frames stream from HBM and a carried batch is never the batch
+being decoded.  One HIP event pair brackets the timed region (both streams join it), so
+``roofline.kernel_avg_us`` is the step period: with overlapping launches a launch's own
+duration is longer than the period at which they complete.
 
 ``--config c3``: the 36-view turntable scan (BASELINE configs[2]) as ONE job, views sharded
 across the ranks (strong scaling): every rank decodes its block, the clouds are gathered to rank
@@ -230,7 +235,7 @@ def main():
     ap.add_argument("--copies", type=int, default=None, help="device copies of each view in the pool")
     ap.add_argument("--batch", type=int, default=None, help="views per fused launch (<= 16)")
     ap.add_argument("--xyz", choices=["f32", "f64"], default="f32")
-    ap.add_argument("--pipeline", choices=["serial", "overlap", "fused", "fused2"], default="fused",
+    ap.add_argument("--pipeline", choices=["serial", "overlap", "fused", "fused2"], default="fused2",
                     help="serial: stats + fused launch per batch on one stream; overlap: the next "
                          "batch's stats on a side stream during this batch's fused launch; fused: "
                          "batch k's fused launch computes batch k+2's histograms; fused2: the same on two "
@@ -459,7 +464,8 @@ def main():
                 "kernel": f"main3_kernel<1,{int(f64)},1,1> (fused decode+triangulate+compaction, {B} views per launch)",
                 "kernel_avg_us": round(kern_avg_s * 1e6, 2),
                 "kernel_time": ("HIP events around each fused launch on its stream" if args.kernel_events == "launch"
-                                else "HIP events around the timed region / steps (gaps included)"),
+                                else "HIP events around the timed region (both launch streams joined) / steps: "
+                                     "the step period, gaps included"),
                 "alg_bytes_per_launch": round(bytes_sum / launches)}
         out = {
             "metric": METRIC,

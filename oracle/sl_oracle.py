@@ -11,9 +11,17 @@ Pinning:
   and the nested ``gray_decode`` / ``reconstruct_point_cloud`` of ``SLSystem.generate_cloud``)
   run in the survey container on rendered captures -> ``tests/golden/*.npz`` made by
   ``tests/golden/make_golden.py``;
-* ``otsu_threshold`` restates OpenCV's ``getThreshVal_Otsu_8u`` (opencv-python, unpinned in
+* ``otsu_threshold`` restates OpenCV's C ``getThreshVal_Otsu_8u`` (opencv-python, unpinned in
   ``requirements.txt:2``, absent from the image).  The reference holds no vectors for it, so
-  it is pinned by exact-rational known-answer tests (``tests/test_oracle_kat.py``);
+  it is pinned by exact-rational known-answer tests (``tests/test_oracle_kat.py``), including
+  the cases an implementation with another evaluation order could resolve differently: exact
+  sigma ties between two splits (sequential fp64 picks the LATER one there) and single
+  non-empty bins at 0 / 255.  opencv-python wheels on x86-64 may dispatch Otsu to IPP's
+  ``ippiComputeThreshold_Otsu``; agreement with that path is PARITY UNPINNED;
+* the numerator ``np.dot(N.T, Oc) + d`` (``server/processing.py:166,219``) is computed with the
+  same ``np.dot`` call, so it carries the host BLAS's gemv rounding exactly as the reference
+  does on that host (for Oc != 0 that rounding differs between BLAS kernels; the Oc != 0
+  fixtures record this host's, ``tests/golden/calib_blas_oc.npz``);
 * the percentile threshold of the legacy variant calls NumPy itself (same library the
   reference calls, ``server/sl_system.py:535``).
 """
