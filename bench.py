@@ -174,6 +174,32 @@ def load_traffic_per_view():
         return None
 
 
+def segments_holding(mask, stride: int, frame_idx) -> int:
+    """64-byte segments of the given frames (frame f at byte f * stride of the stack) that hold a
+    valid pixel, summed over the frames: the pattern bytes a mask-first decode must read.  A lane's
+    8-byte load never straddles a segment (lanes start at multiples of 8 px, stride % 16 == 0).
+    `mask` is a flat torch bool tensor of the view's pixels."""
+    import torch
+    idx = torch.nonzero(mask.reshape(-1)).reshape(-1).to(torch.int64)
+    total = 0
+    for f in frame_idx:
+        total += int(torch.unique((idx + f * stride) >> 6).numel())
+    return total
+
+
+def mask_first_segments(frames, cfg, H, W, dev) -> int:
+    """`segments_holding` of one device view's pattern frames, its mask from the maps path."""
+    from structured_light_for_3d_model_replication_amd import engine as E
+    rec = mask_first_segments.__dict__.setdefault("rec", {}).get((H, W))
+    if rec is None:
+        rec = mask_first_segments.rec[(H, W)] = E.Reconstructor(H, W, device=dev)
+    _, _, mask = rec.decode(frames, cfg)
+    n = min(frames.n_frames, 2 + 2 * (cfg.n_sets_col + cfg.n_sets_row))   # frames the plan reads
+    if frames.stride % 64 == 0:          # every frame's segments line up: one count per frame
+        return (n - 2) * segments_holding(mask != 0, frames.stride, [0])
+    return segments_holding(mask != 0, frames.stride, range(2, n))
+
+
 RESULT_OUT = sys.stdout          # main() points it at the original stdout
 
 
@@ -336,6 +362,7 @@ def main():
         s_main.synchronize()
         pts += [int(clouds[0][k].count.item()) for k in range(B)]
     pts = pts[:P]
+    seg_frames = [mask_first_segments(dframes[v], cfg, H, W, dev) for v in range(P)]
 
     K, Wm = args.steps, args.warmup
     # the whole run as ONE batch stream: warmup + timed + 2 look-ahead batches whose thresholds
@@ -356,7 +383,12 @@ def main():
         return [(b * B + k) % P for k in range(B)]
 
     total_pts = sum(pts[v] for b in range(Wm, Wm + K) for v in pool_views(b))
-    bytes_alg = sum(frame_b + out_b * pts[v] for b in range(Wm, Wm + K) for v in pool_views(b))
+    # algorithmic bytes of the mask-first decode (SLG_MASK_FIRST): white + black of every pixel,
+    # each pattern frame's 64-byte segments that hold a valid pixel, 18 B per point; and the
+    # dense figure (every frame byte) beside it
+    wb_b = 2 * H * W
+    bytes_alg = sum(wb_b + 64 * seg_frames[v] + out_b * pts[v] for b in range(Wm, Wm + K) for v in pool_views(b))
+    bytes_dense = sum(frame_b + out_b * pts[v] for b in range(Wm, Wm + K) for v in pool_views(b))
 
     def run_range(lo, hi, events=None):
         if args.pipeline in ("overlap", "fused", "fused2"):
@@ -439,16 +471,16 @@ def main():
         if not (same and counts_ok and oracle_ok):
             log(f"[rank {rank}] VERIFY FAILED: {verify}")
 
-    stats = torch.tensor([dt, float(total_pts), kern_ms, bytes_alg], dtype=torch.float64, device=dev)
+    stats = torch.tensor([dt, float(total_pts), kern_ms, bytes_alg, bytes_dense], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = stats[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         sums = stats[1:].clone()
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
         dt_max = float(tmax.item())
-        all_pts, kern_sum, bytes_sum = (float(x) for x in sums.tolist())
+        all_pts, kern_sum, bytes_sum, dense_sum = (float(x) for x in sums.tolist())
     else:
-        dt_max, all_pts, kern_sum, bytes_sum = dt, float(total_pts), kern_ms, bytes_alg
+        dt_max, all_pts, kern_sum, bytes_sum, dense_sum = dt, float(total_pts), kern_ms, bytes_alg, bytes_dense
 
     if rank == 0:
         launches = K * world
@@ -466,7 +498,13 @@ def main():
                 "kernel_time": ("HIP events around each fused launch on its stream" if args.kernel_events == "launch"
                                 else "HIP events around the timed region (both launch streams joined) / steps: "
                                      "the step period, gaps included"),
-                "alg_bytes_per_launch": round(bytes_sum / launches)}
+                "alg_bytes_per_launch": round(bytes_sum / launches),
+                "alg_bytes": "mask-first decode: white + black of every pixel, the 64-B segments of each "
+                             "pattern frame that hold a valid pixel, 18 B per point (3 B texture, 12 B XYZ, 3 B BGR)",
+                "dense_bytes_per_launch": round(dense_sum / launches),
+                "dense_frac": round(dense_sum / launches / kern_avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                "dense": "SURVEY 8(d)'s figure (every frame byte once + 18 B per point) over the same time: the "
+                         "HBM rate a decode that reads every frame would need to match this step time"}
         out = {
             "metric": METRIC,
             "value": round(all_pts / dt_max / 1e6, 2),

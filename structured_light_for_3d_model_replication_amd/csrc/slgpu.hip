@@ -748,15 +748,36 @@ __device__ inline uint2 ld_frame8(const MainParams& p, int frame, int64_t lp) {
 // `tail` (wave-uniform) is set only in the last tile, where map/texture reads need guards;
 // frame reads never do: the frame stride is >= round_up(H*W, 8) and out-of-image lanes read
 // pixel 0 (their mask bits are cleared).
-template <int ROW_MODE, int SRC_FRAMES, int kBatch>
+// MF (mask first, the fused reconstruction only): the mask is computed from white / black before
+// any pattern frame is read, and a lane none of whose 8 pixels is valid reads no pattern frame at
+// all (its codes are never used: the reference masks them out, processing.py:121-124,157).  The
+// memory system then fetches only the 64-byte segments a valid pixel lies in.  `pre()` runs once
+// the lane is known to hold a valid pixel, before its pattern loads (the texture loads).
+struct NoPre {
+  __device__ void operator()() const {}
+};
+
+template <int ROW_MODE, int SRC_FRAMES, int kBatch, bool MF = false, class Pre = NoPre>
 __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, uint32_t& valid,
-                                   int (&col)[kPx], int (&row)[kPx]) {
+                                   int (&col)[kPx], int (&row)[kPx], Pre pre = Pre()) {
   valid = 0;
   if (SRC_FRAMES) {
     const int smin = p.ws->smin, cmin = p.ws->cmin;
     const int64_t lp = px0 < p.n_px ? px0 : 0;
     const uint2 w = ld_frame8(p, 0, lp);
     const uint2 bl = ld_frame8(p, 1, lp);
+    if constexpr (MF) {
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {
+        const int wv = ((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 0xff;
+        const int bv = ((k < 4 ? bl.x : bl.y) >> (8 * (k & 3))) & 0xff;
+        valid |= uint32_t((wv >= smin) & ((wv - bv) >= cmin) & (px0 + k < p.n_px)) << k;
+        col[k] = 0;
+        row[k] = 0;
+      }
+      if (valid == 0u) return;
+      pre();
+    }
     PlaneAcc qc = {{0, 0}, {0, 0}}, qr = {{0, 0}, {0, 0}};
     const int np_r = ROW_MODE != 0 ? p.row_pairs : 0;
     // compile-time trip count (kMaxBits pairs max), fully unrolled: only forward, wave-uniform
@@ -794,9 +815,11 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
     acc_codes(qr, np_r, p.row_pre, p.row_post, ar);
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
-      const int wv = ((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 0xff;
-      const int bv = ((k < 4 ? bl.x : bl.y) >> (8 * (k & 3))) & 0xff;
-      valid |= uint32_t((wv >= smin) & ((wv - bv) >= cmin) & (px0 + k < p.n_px)) << k;
+      if constexpr (!MF) {
+        const int wv = ((k < 4 ? w.x : w.y) >> (8 * (k & 3))) & 0xff;
+        const int bv = ((k < 4 ? bl.x : bl.y) >> (8 * (k & 3))) & 0xff;
+        valid |= uint32_t((wv >= smin) & ((wv - bv) >= cmin) & (px0 + k < p.n_px)) << k;
+      }
       col[k] = unpack_code(ac, k);
       row[k] = ROW_MODE != 0 ? unpack_code(ar, k) : 0;
     }
@@ -1272,6 +1295,9 @@ constexpr int kMaxViews = 16;
 #define SLG_TEX_LATE 1                     // texture bytes read only by lanes with a valid pixel, after the
                                            // decode (285.1 vs 289.7 us per 12-view launch, profiles/r3d/ab.log)
 #endif
+#ifndef SLG_MASK_FIRST
+#define SLG_MASK_FIRST 1                   // decode_lane MF: pattern frames read only where a pixel is valid
+#endif
 #ifndef SLG_M3_WAVES
 #define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
 #endif
@@ -1565,13 +1591,19 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
           if (px0 * 3 + k < p.n_px * 3) tex[k >> 2] |= uint32_t(p.texture[px0 * 3 + k]) << (8 * (k & 3));
       }
     };
-    if (!SLG_TEX_LATE) load_tex();
+    constexpr bool MF = SLG_MASK_FIRST && SRC_FRAMES;
+    if (!SLG_TEX_LATE && !MF) load_tex();
     uint32_t valid;
     int col[kPx], row[kPx];
-    decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH>(p, px0, tail, valid, col, row);
+    if constexpr (MF) {
+      // mask first: a lane with a valid pixel issues its texture loads, then its pattern loads
+      decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH, true>(p, px0, tail, valid, col, row, load_tex);
+    } else {
+      decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH>(p, px0, tail, valid, col, row);
+    }
     // SLG_TEX_LATE: only lanes with a valid pixel read their 24 texture bytes, once the mask is
     // known (the block scan's barrier covers part of the latency)
-    if (SLG_TEX_LATE && valid != 0u) load_tex();
+    if (!MF && SLG_TEX_LATE && valid != 0u) load_tex();
     const int2 sc = block_scan(__popc(valid), s_wtot);
     n_items = sc.y;
     int m = sc.x;
