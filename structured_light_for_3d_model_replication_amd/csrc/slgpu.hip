@@ -757,7 +757,12 @@ struct NoPre {
   __device__ void operator()() const {}
 };
 
-template <int ROW_MODE, int SRC_FRAMES, int kBatch, bool MF = false, class Pre = NoPre>
+// PLAN: (col_pairs << 4) | row_pairs as compile-time constants (main3's specialised instances for
+// the common capture layouts, kPlans), or 0: the counts come from the view's plan at run time.
+// Constant counts make every frame load unconditional, so the decode consumes each pair as it
+// lands (vmcnt(n) in issue order) instead of after a vmcnt(0) for the whole batch, and drop the
+// per-pair branches (243.3 vs 259.8 us per 12-view launch, profiles/r3m).
+template <int ROW_MODE, int SRC_FRAMES, int kBatch, bool MF = false, int PLAN = 0, class Pre = NoPre>
 __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, uint32_t& valid,
                                    int (&col)[kPx], int (&row)[kPx], Pre pre = Pre()) {
   valid = 0;
@@ -779,7 +784,8 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
       pre();
     }
     PlaneAcc qc = {{0, 0}, {0, 0}}, qr = {{0, 0}, {0, 0}};
-    const int np_r = ROW_MODE != 0 ? p.row_pairs : 0;
+    const int np_c = PLAN ? (PLAN >> 4) : p.col_pairs;
+    const int np_r = ROW_MODE == 0 ? 0 : (PLAN ? (PLAN & 15) : p.row_pairs);
     // compile-time trip count (kMaxBits pairs max), fully unrolled: only forward, wave-uniform
     // branches remain, so the loads of a batch stay in flight together (no vmcnt(0) per load)
 #pragma unroll
@@ -787,7 +793,7 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
       uint2 cp[kBatch], ci[kBatch], rp[kBatch], ri[kBatch];
 #pragma unroll
       for (int g = 0; g < kBatch; ++g)
-        if (b0 + g < p.col_pairs) {
+        if (b0 + g < np_c) {
           cp[g] = ld_frame8(p, p.col_first + 2 * (b0 + g), lp);
           ci[g] = ld_frame8(p, p.col_first + 2 * (b0 + g) + 1, lp);
         }
@@ -799,7 +805,7 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
         }
 #pragma unroll
       for (int g = 0; g < kBatch; ++g)
-        if (b0 + g < p.col_pairs) {
+        if (b0 + g < np_c) {
           if (b0 + g < 8) acc_pair<false>(qc, cp[g], ci[g]);
           else acc_pair<true>(qc, cp[g], ci[g]);
         }
@@ -811,7 +817,7 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
         }
     }
     uint32_t ac[4], ar[4];
-    acc_codes(qc, p.col_pairs, p.col_pre, p.col_post, ac);
+    acc_codes(qc, np_c, p.col_pre, p.col_post, ac);
     acc_codes(qr, np_r, p.row_pre, p.row_post, ar);
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
@@ -1518,7 +1524,7 @@ __device__ inline void tri_rounds(const MainParams& p, int i, int n_items, const
 
 // PROF: the profiling instance (SLG_DBG set): honours the ablation bits of MainParams::dbg and
 // writes per-workgroup phase records; the production instances carry none of that code.
-template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS, bool PROF>
+template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS, bool PROF, int PLAN = 0>
 __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) void main3_kernel(Main3Params P) {
   using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
   constexpr int NS = ROW_MODE == 2 ? 2 : 1;
@@ -1597,9 +1603,9 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     int col[kPx], row[kPx];
     if constexpr (MF) {
       // mask first: a lane with a valid pixel issues its texture loads, then its pattern loads
-      decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH, true>(p, px0, tail, valid, col, row, load_tex);
+      decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH, true, PLAN>(p, px0, tail, valid, col, row, load_tex);
     } else {
-      decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH>(p, px0, tail, valid, col, row);
+      decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH, false, PLAN>(p, px0, tail, valid, col, row);
     }
     // SLG_TEX_LATE: only lanes with a valid pixel read their 24 texture bytes, once the mask is
     // known (the block scan's barrier covers part of the latency)
@@ -2104,12 +2110,32 @@ using Main3Fn = void (*)(Main3Params);
 // Production instances for every (row_mode, xyz, source, ray) case; the profiling instance
 // (SLG_DBG with any main3 bit) exists for the benchmark shape only: row_mode 1, f32 XYZ, frames,
 // pinhole rays (tools/kbench.py).
+// Decode plans main3 has specialised instances for (PLAN = (col_pairs << 4) | row_pairs), with
+// row_mode 1 or 2 and pinhole rays: C2's 11 + 10 bits (1920x1080 projector, row_scale 2), the
+// reference's default 11 + 11 (processing.py:29-30; C3, C5) and C4's 12 + 12.
+#define SLG_PLAN_C2 0xBA
+#define SLG_PLAN_1080P 0xBB
+#define SLG_PLAN_C4 0xCC
+
 template <int SRC>
-Main3Fn pick_main(int row_mode, int x64, int rays) {
-  if (debug_flags() & kMainDbgBits)
-    return (SRC == 1 && row_mode == 1 && x64 == 0 && rays == SLG_RAYS_PINHOLE) ? main3_kernel<1, 0, 1, 1, true> : nullptr;
+Main3Fn pick_main(int row_mode, int x64, int rays, int plan = 0) {
+  if (debug_flags() & kMainDbgBits) {
+    if (!(SRC == 1 && row_mode == 1 && x64 == 0 && rays == SLG_RAYS_PINHOLE)) return nullptr;
+    return plan == SLG_PLAN_C2 ? main3_kernel<1, 0, 1, 1, true, SLG_PLAN_C2> : main3_kernel<1, 0, 1, 1, true>;
+  }
+#ifndef SLG_FAST_BUILD
+  if (SRC == 1 && rays == SLG_RAYS_PINHOLE && row_mode != 0) {
+#define SLG_PCASE(RM, X, PL) if (row_mode == RM && x64 == X && plan == PL) return main3_kernel<RM, X, 1, 1, false, PL>;
+    SLG_PCASE(1, 0, SLG_PLAN_C2) SLG_PCASE(1, 1, SLG_PLAN_C2)
+    SLG_PCASE(1, 0, SLG_PLAN_1080P) SLG_PCASE(1, 1, SLG_PLAN_1080P)
+    SLG_PCASE(1, 0, SLG_PLAN_C4) SLG_PCASE(1, 1, SLG_PLAN_C4)
+#undef SLG_PCASE
+  }
+#endif
 #define SLG_CASE(RM, X, R) if (row_mode == RM && x64 == X && rays == R) return main3_kernel<RM, X, SRC, R, false>;
 #ifdef SLG_FAST_BUILD   // register/spill inspection builds only: the benchmark's instance alone
+  if (plan == SLG_PLAN_C2 && row_mode == 1 && x64 == 0 && rays == SLG_RAYS_PINHOLE && SRC == 1)
+    return main3_kernel<1, 0, 1, 1, false, SLG_PLAN_C2>;
   SLG_CASE(1, 0, 1)
   return nullptr;
 #endif
@@ -2208,9 +2234,16 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
   rc = fill_calib(mp.c, calib, tp, n_px, caps[0].width);
   if (rc) return rc;
   mp.c.n_tiles = n_tiles_of(n_px);
-  const Main3Fn fn = pick_main<1>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode);
   for (int v0 = 0, launch = 0; v0 < n_views; v0 += kMaxViews, ++launch) {
     mp.n_views = n_views - v0 < kMaxViews ? n_views - v0 : kMaxViews;
+    int plan = -1;                                  // the views' common pair counts, else 0
+    for (int k = 0; k < mp.n_views; ++k) {
+      Plan pl;
+      make_plan(&caps[v0 + k], dp, &pl);
+      const int key = pl.col_pairs <= 15 && pl.row_pairs <= 15 ? (pl.col_pairs << 4) | pl.row_pairs : 0;
+      plan = plan < 0 || plan == key ? key : 0;
+    }
+    const Main3Fn fn = pick_main<1>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode, plan < 0 ? 0 : plan);
     for (int k = 0; k < mp.n_views; ++k) {
       const int v = v0 + k;
       ViewIO& io = mp.v[k];

@@ -93,10 +93,13 @@ def test_c2_bench_launch_shape(mods, scan):
     assert min(len(w[0]) for w in want) > 500_000
 
 
-def test_c2_two_stream_pipeline(mods, scan):
+@pytest.mark.parametrize("bv", [6, 16])
+def test_c2_two_stream_pipeline(mods, scan, bv):
     """bench.py --pipeline fused2: batch k on stream k % 2 (launches overlap), launch k carrying
-    batch k+4's histograms and finishing batch k+2's thresholds, 4 slots; 6-view batches over
-    the 36 views, issued in two pieces.  Every count against the oracle, clouds on a subset."""
+    batch k+4's histograms and finishing batch k+2's thresholds, 4 slots; bv-view batches over
+    the 36 views taken cyclically (16: the bench's launch, 7 batches so launches carry and
+    finish at that width too), issued in two pieces.  Every count against the oracle, clouds on
+    a subset."""
     E, N = mods
     import torch
     cal, views = scan
@@ -104,22 +107,25 @@ def test_c2_two_stream_pipeline(mods, scan):
     dev = [E.DeviceFrames(list(v.frames), v.texture) for v in views]
     dcal = E.DeviceCalib(cal, 1080, 1920)
     cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
-    eng = E.BatchReconstructor(1080, 1920, 6, slots=4)
-    clouds = [E.Cloud(1920 * 1080, 1, False) for _ in range(N_VIEWS)]
-    batches = [eng.prepare(dev[6 * b:6 * b + 6], cfg, dcal, clouds[6 * b:6 * b + 6], 1, 2.0, slot=b % 4)
-               for b in range(6)]
+    eng = E.BatchReconstructor(1080, 1920, bv, slots=4)
+    nb = max(6, (N_VIEWS + bv - 1) // bv) if bv < 16 else 7
+    idx = [(bv * b + k) % N_VIEWS for b in range(nb) for k in range(bv)]
+    clouds = [E.Cloud(1920 * 1080, 1, False) for _ in idx]
+    batches = [eng.prepare([dev[i] for i in idx[bv * b:bv * b + bv]], cfg, dcal, clouds[bv * b:bv * b + bv], 1, 2.0,
+                           slot=b % 4) for b in range(nb)]
     s0, s1 = torch.cuda.Stream(), torch.cuda.Stream()
-    eng.run_pipelined(batches, s0, s1, mode="fused2", start=0, stop=2)
+    eng.run_pipelined(batches, s0, s1, mode="fused2", start=0, stop=nb // 2)
     torch.cuda.synchronize()
-    eng.run_pipelined(batches, s0, s1, mode="fused2", start=2, stop=6)
+    eng.run_pipelined(batches, s0, s1, mode="fused2", start=nb // 2, stop=nb)
     torch.cuda.synchronize()
-    for k, (c, (Po, Co)) in enumerate(zip(clouds, want)):
+    for k, (c, i) in enumerate(zip(clouds, idx)):
+        Po, Co = want[i]
         P, C = c.result()
         assert P.shape[0] == Po.shape[0], (k, P.shape[0], Po.shape[0])
         if k % 5 == 0:
             assert np.array_equal(C.cpu().numpy(), Co), k
             _xyz32_close(P.cpu().numpy(), Po)
-    assert all(eng.header(s, v)[3084:3088].cpu().numpy()[0] & 1 == 0 for s in range(4) for v in range(6))
+    assert all(eng.header(s, v)[3084:3088].cpu().numpy()[0] & 1 == 0 for s in range(4) for v in range(bv))
 
 
 def test_c3_sharded_job(mods, scan):

@@ -49,12 +49,13 @@ __device__ inline void ldw(const uint8_t* base, uint32_t off, uint32_t soff, uin
 }
 
 // MODE 0 dense, 1 mf, 2 mf_l2.  W: dwords per lane (2: 8 px, 4: 16 px).
-template <int W, int BLOCK, int MODE, int STORE>
-__global__ __launch_bounds__(BLOCK) void probe(const uint8_t* frames, int64_t view_bytes, int tiles_per_view,
+template <int W, int BLOCK, int MODE, int STORE, int TAIL = 0, int LDS_KB = 0, int WAVES = 1>
+__global__ __launch_bounds__(BLOCK, WAVES) void probe(const uint8_t* frames, int64_t view_bytes, int tiles_per_view,
                                                const uint8_t* lane_valid, uint32_t* sink, float* xyz, uint8_t* bgr) {
   constexpr int PX = 4 * W;
   constexpr int TILE = BLOCK * PX;
   __shared__ int s_wtot[BLOCK / 64];
+  __shared__ uint32_t s_pad[LDS_KB > 0 ? LDS_KB * 256 : 1];   // occupancy: LDS per workgroup
   const int view = blockIdx.x / tiles_per_view, tile = blockIdx.x - view * tiles_per_view;
   const uint8_t* f = frames + view * view_bytes;
   int64_t px0 = int64_t(tile) * TILE + int64_t(threadIdx.x) * PX;
@@ -109,6 +110,20 @@ __global__ __launch_bounds__(BLOCK) void probe(const uint8_t* frames, int64_t vi
     for (int j = 0; j < 2 * W; ++j) h += gray2bin_x2(ac[j]) * 3u + gray2bin_x2(ar[j]);
   }
   h ^= valid;
+  if constexpr (TAIL > 0) {
+    // stand-in for phases B-D: TAIL rounds of 4 independent fp64 fma chains (a lane's items)
+    double a0 = h, a1 = h + 1, a2 = h + 2, a3 = h + 3;
+    for (int i = 0; i < TAIL; ++i) {
+      a0 = __builtin_fma(a0, 1.0000001, 0.5); a1 = __builtin_fma(a1, 1.0000001, 0.5);
+      a2 = __builtin_fma(a2, 1.0000001, 0.5); a3 = __builtin_fma(a3, 1.0000001, 0.5);
+    }
+    h += uint32_t(a0 + a1 + a2 + a3);
+  }
+  if constexpr (LDS_KB > 0) {
+    s_pad[threadIdx.x] = h;
+    __syncthreads();
+    h += s_pad[(threadIdx.x + 64) % BLOCK];
+  }
   if constexpr (STORE) {
     // compacted per workgroup: this lane's valid pixels at its block-scan offset
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -145,7 +160,7 @@ __global__ void fill(uint8_t* p, int64_t n, uint32_t seed) {
 
 static double g_pattern_bytes[2];   // [W == 4] pattern bytes a view needs at 64-B segments
 
-template <int W, int BLOCK, int MODE, int STORE>
+template <int W, int BLOCK, int MODE, int STORE, int TAIL = 0, int LDS_KB = 0, int WAVES = 1>
 void run(const char* name, const uint8_t* frames, int n_views, const uint8_t* lane_valid, uint32_t* sink,
          float* xyz, uint8_t* bgr, int64_t vb) {
   constexpr int TILE = BLOCK * 4 * W;
@@ -155,7 +170,7 @@ void run(const char* name, const uint8_t* frames, int n_views, const uint8_t* la
   std::vector<float> ts;
   for (int it = 0; it < 40; ++it) {
     CK(hipEventRecord(a, 0));
-    hipLaunchKernelGGL((probe<W, BLOCK, MODE, STORE>), dim3(tpv * n_views), dim3(BLOCK), 0, 0, frames, vb, tpv,
+    hipLaunchKernelGGL((probe<W, BLOCK, MODE, STORE, TAIL, LDS_KB, WAVES>), dim3(tpv * n_views), dim3(BLOCK), 0, 0, frames, vb, tpv,
                        lane_valid, sink, xyz, bgr);
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
@@ -215,15 +230,29 @@ int main(int argc, char** argv) {
   for (int64_t i = 0; i < kNpx; ++i) nv += mask[i] != 0;
   printf("mask: %.4f of pixels valid; pattern segments needed %.4f (8 px lanes) %.4f (16 px lanes)\n",
          double(nv) / kNpx, g_pattern_bytes[0] / (42.0 * kNpx), g_pattern_bytes[1] / (42.0 * kNpx));
+  const char* only = getenv("MF_PROBE_ONLY");
+  if (!only || only[0] != 't') {
+    for (int rep = 0; rep < 2; ++rep) {
+      run<2, 512, 0, 0>("dense  8px blk512", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+      run<2, 512, 1, 0>("mf     8px blk512", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+      run<2, 512, 2, 0>("mf_l2  8px blk512", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+      run<4, 256, 1, 0>("mf16  16px blk256", frames, n_views, d_lv16, sink, xyz, bgr, vb);
+      run<4, 256, 2, 0>("mf16_l2 16px blk256", frames, n_views, d_lv16, sink, xyz, bgr, vb);
+      run<2, 512, 1, 1>("mf     8px blk512 + stores", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+      run<2, 512, 2, 1>("mf_l2  8px blk512 + stores", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+      run<2, 512, 0, 1>("dense  8px blk512 + stores", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+    }
+  }
+  // occupancy vs a compute tail: 2 workgroups per CU (70 KB LDS each) against 3 (50 KB), a
+  // tail of 0 / 150 / 300 rounds of 4 fp64 fma chains (~ phases B-D of main3: 600-1200 VALU)
   for (int rep = 0; rep < 2; ++rep) {
-    run<2, 512, 0, 0>("dense  8px blk512", frames, n_views, d_lv8, sink, xyz, bgr, vb);
-    run<2, 512, 1, 0>("mf     8px blk512", frames, n_views, d_lv8, sink, xyz, bgr, vb);
-    run<2, 512, 2, 0>("mf_l2  8px blk512", frames, n_views, d_lv8, sink, xyz, bgr, vb);
-    run<4, 256, 1, 0>("mf16  16px blk256", frames, n_views, d_lv16, sink, xyz, bgr, vb);
-    run<4, 256, 2, 0>("mf16_l2 16px blk256", frames, n_views, d_lv16, sink, xyz, bgr, vb);
-    run<2, 512, 1, 1>("mf     8px blk512 + stores", frames, n_views, d_lv8, sink, xyz, bgr, vb);
-    run<2, 512, 2, 1>("mf_l2  8px blk512 + stores", frames, n_views, d_lv8, sink, xyz, bgr, vb);
-    run<2, 512, 0, 1>("dense  8px blk512 + stores", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+    run<2, 512, 1, 0, 0, 70, 4>("mf tail0   2 WG/CU", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+    run<2, 512, 1, 0, 0, 50, 6>("mf tail0   3 WG/CU", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+    run<2, 512, 1, 0, 150, 70, 4>("mf tail150 2 WG/CU", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+    run<2, 512, 1, 0, 150, 50, 6>("mf tail150 3 WG/CU", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+    run<2, 512, 1, 0, 300, 70, 4>("mf tail300 2 WG/CU", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+    run<2, 512, 1, 0, 300, 50, 6>("mf tail300 3 WG/CU", frames, n_views, d_lv8, sink, xyz, bgr, vb);
+    run<2, 512, 1, 0, 300, 35, 8>("mf tail300 4 WG/CU", frames, n_views, d_lv8, sink, xyz, bgr, vb);
   }
   return 0;
 }
