@@ -876,8 +876,6 @@ struct TriOut {
 // Ray-plane intersection of one valid pixel (processing.py:143-234), fp64 in NumPy's order, in
 // three parts so phase B can issue an item's plane gathers, compute its ray while they are in
 // flight, and only then combine (tri_item chains them for the other callers).
-// NOG (profiling ablations, SLG_DBG bits 10-13): 1 column planes from registers, 2 row planes
-// from registers, 4 column gathers from one broadcast address, 8 row gathers likewise.
 struct TriPlanes {
   double2 pc01, pc23;  // column plane: (n0, n1), (n2, d or numer)
   double2 pr01, pr23;  // row plane (row_mode 1/2)
@@ -888,14 +886,11 @@ struct TriPlanes {
 // then read consecutive 16-byte pairs (8 per cache line) instead of every other 16 bytes of
 // 32-byte rows.
 // NP: 0 reads p.num_pre at run time, 1 / 2 take it as set / clear (phase B picks per workgroup).
-template <int NOG = 0, int NP = 0>
+template <int NP = 0>
 __device__ inline void tri_planes_col(const MainParams& p, uint32_t code, double2& pc01, double2& pc23) {
-  if constexpr ((NOG & 1) != 0) {
-    pc01 = make_double2(double(code & 0xffffu) * p.rfx, p.rfy);
-    pc23 = make_double2(p.rfx, double(code >> 16) * p.rfy);
-  } else if (NP == 1 || (NP == 0 && p.num_pre)) {
+  if (NP == 1 || (NP == 0 && p.num_pre)) {
     const double2* qc = reinterpret_cast<const double2*>(p.pcol);
-    const uint32_t cc = (NOG & 4) ? (code & 1u) : (code & 0xffffu);
+    const uint32_t cc = code & 0xffffu;
     pc01 = qc[cc];
     pc23 = qc[p.n_pcol + cc];
   } else {
@@ -905,18 +900,11 @@ __device__ inline void tri_planes_col(const MainParams& p, uint32_t code, double
   }
 }
 
-template <int ROW_MODE, int NOG = 0, int NP = 0>
+template <int ROW_MODE, int NP = 0>
 __device__ inline void tri_planes_row(const MainParams& p, uint32_t code, double2& pr01, double2& pr23) {
   pr01 = make_double2(0, 0);
   pr23 = make_double2(0, 0);
-  if constexpr ((NOG & 2) != 0) {
-    pr01 = make_double2(double(code >> 16) * p.rfy, p.rfx);
-    pr23 = make_double2(p.rfy, -2.0);
-  } else if constexpr ((NOG & 8) != 0 && ROW_MODE == 1) {
-    const double2* qr = reinterpret_cast<const double2*>(p.prow + 4 * int64_t(code >> 31));
-    pr01 = qr[0];
-    pr23 = qr[1];
-  } else if constexpr (ROW_MODE == 2) {
+  if constexpr (ROW_MODE == 2) {
     if (NP == 1 || (NP == 0 && p.num_pre)) {
       const double2* qr = reinterpret_cast<const double2*>(p.prow);
       pr01 = qr[code >> 16];
@@ -933,11 +921,11 @@ __device__ inline void tri_planes_row(const MainParams& p, uint32_t code, double
   }
 }
 
-template <int ROW_MODE, int NOG = 0, int NP = 0>
+template <int ROW_MODE, int NP = 0>
 __device__ inline TriPlanes tri_planes(const MainParams& p, uint32_t code) {
   TriPlanes t;
-  tri_planes_col<NOG, NP>(p, code, t.pc01, t.pc23);
-  tri_planes_row<ROW_MODE, NOG, NP>(p, code, t.pr01, t.pr23);
+  tri_planes_col<NP>(p, code, t.pc01, t.pc23);
+  tri_planes_row<ROW_MODE, NP>(p, code, t.pr01, t.pr23);
   return t;
 }
 
@@ -1474,7 +1462,7 @@ __device__ inline int bgr_slot(int m) { return m + (m >> SLG_BGR_PAD); }
 // Phase B of main3 for rounds [i, i + G) (item m = tid + 256 * round), FAST path: the G items'
 // loads and fp64 chains are independent, so their plane gathers are in flight together.
 // tri_rounds: i is a compile-time multiple of G (the unrolled group loop); tri_rounds_at: any i.
-template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NOG = 0, int NP = 0>
+template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NP = 0>
 __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, const uint2* s_item,
                                      XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
   const int tid = threadIdx.x;
@@ -1491,7 +1479,7 @@ __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, co
     const uint32_t sc = it.x, suv = it.y;
     const uint32_t code = in[h] ? sc : 0u;
     uvs[h] = in[h] ? suv : 0u;
-    pl[h] = tri_planes<ROW_MODE, NOG, NP>(p, code);
+    pl[h] = tri_planes<ROW_MODE, NP>(p, code);
   }
 #pragma unroll
   for (int h = 0; h < G; ++h)                      // ... while the rays are computed
@@ -1516,10 +1504,10 @@ __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, co
   }
 }
 
-template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NOG = 0, int NP = 0>
+template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NP = 0>
 __device__ inline void tri_rounds(const MainParams& p, int i, int n_items, const uint2* s_item,
                                   XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
-  tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_item, pts, km);
+  tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt, NP>(p, i, n_items, s_item, pts, km);
 }
 
 // PROF: the profiling instance (SLG_DBG set): honours the ablation bits of MainParams::dbg and
@@ -1567,11 +1555,15 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // carried, whose partials live there).
   const bool prof = PROF && (p.dbg & 64) != 0;
   uint64_t t_phase = prof ? __builtin_amdgcn_s_memrealtime() : 0;
-  uint32_t rec[8] = {0, 0, 0, 0, 0, 0, 0, uint32_t(t_phase)};   // [7]: start time (low 32 bits)
+  // the record lives in LDS (tid 0 writes it): as a register array it pushed the profiling
+  // instance into VGPR spills once the production decode reached the register limit
+  __shared__ uint32_t s_rec[8];
+  if (prof && tid == 0) s_rec[7] = uint32_t(t_phase);                // start time (low 32 bits)
+  uint32_t polls = 0, naps = 0;
   auto stamp = [&](int k) {
     if (prof && tid == 0) {
       const uint64_t t = __builtin_amdgcn_s_memrealtime();
-      rec[k] = uint32_t(t - t_phase);
+      s_rec[k] = uint32_t(t - t_phase);
       t_phase = t;
     }
   };
@@ -1647,36 +1639,27 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     // then a single round, so no empty round is computed.
     const int rounds = (n_items + kB - 1) / kB;
     int i = 0;
-    auto all_rounds = [&](auto nog, auto np) {
-      constexpr int NOG = decltype(nog)::value;
+    auto all_rounds = [&](auto np) {
       constexpr int NP = decltype(np)::value;
 #pragma unroll
       for (int g = 0; g + SLG_TRI_GROUP <= kIt; g += SLG_TRI_GROUP)
         if (i + SLG_TRI_GROUP <= rounds) {
-          tri_rounds<SLG_TRI_GROUP, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, g, n_items, s_item, pts, km);
+          tri_rounds<SLG_TRI_GROUP, ROW_MODE, RAYS, XT, NS, kIt, NP>(p, g, n_items, s_item, pts, km);
           i = g + SLG_TRI_GROUP;
         }
       if (SLG_TRI_GROUP > 2 && i + 2 <= rounds) {
-        tri_rounds_at<2, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_item, pts, km);
+        tri_rounds_at<2, ROW_MODE, RAYS, XT, NS, kIt, NP>(p, i, n_items, s_item, pts, km);
         i += 2;
       }
       if (i < rounds) {
-        tri_rounds_at<1, ROW_MODE, RAYS, XT, NS, kIt, NOG, NP>(p, i, n_items, s_item, pts, km);
+        tri_rounds_at<1, ROW_MODE, RAYS, XT, NS, kIt, NP>(p, i, n_items, s_item, pts, km);
         i += 1;
       }
     };
-    const int nog = PROF ? (p.dbg >> 10) & 15 : 0;   // profiling ablations of the plane gathers
-    using NP0 = std::integral_constant<int, 0>;
-    if (PROF && nog == 3) all_rounds(std::integral_constant<int, PROF ? 3 : 0>(), NP0());
-    else if (PROF && nog == 1) all_rounds(std::integral_constant<int, PROF ? 1 : 0>(), NP0());
-    else if (PROF && nog == 2) all_rounds(std::integral_constant<int, PROF ? 2 : 0>(), NP0());
-    else if (PROF && nog == 4) all_rounds(std::integral_constant<int, PROF ? 4 : 0>(), NP0());
-    else if (PROF && nog == 8) all_rounds(std::integral_constant<int, PROF ? 8 : 0>(), NP0());
-    else if (PROF && nog == 12) all_rounds(std::integral_constant<int, PROF ? 12 : 0>(), NP0());
     // numerator tables or not: a block-uniform choice between two straight-line instances,
     // so neither computes the other's numerator and selects
-    else if (p.num_pre) all_rounds(NP0(), std::integral_constant<int, 1>());
-    else all_rounds(NP0(), std::integral_constant<int, 2>());
+    if (p.num_pre) all_rounds(std::integral_constant<int, 1>());
+    else all_rounds(std::integral_constant<int, 2>());
 #pragma unroll
     for (int r = 0; r < kIt; ++r)
       if (r >= i) {
@@ -1744,8 +1727,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       uint64_t* st = p.states + int64_t(s) * tiles;
       uint64_t excl;
       int ht;
-      while (!(SLG_SCALAR_LB ? lookback_scalar<PROF>(p, st, tile, agg, excl, ht, rec[4], rec[5])
-                             : lookback_try<PROF>(p, st, tile, agg, excl, ht, rec[4], rec[5]))) {
+      while (!(SLG_SCALAR_LB ? lookback_scalar<PROF>(p, st, tile, agg, excl, ht, polls, naps)
+                             : lookback_try<PROF>(p, st, tile, agg, excl, ht, polls, naps))) {
         // a predecessor has not published for long (it may not be dispatched yet): publish
         // its aggregate for it, computed by this wave, and look back again
         const int hagg = tile_keep_count_wave<ROW_MODE, SRC_FRAMES, RAYS>(p, ht, s);
@@ -1805,10 +1788,10 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     __syncthreads();
     stamp(3);
     if (tid == 0) {
-      rec[6] = uint32_t(n_items);
+      s_rec[4] = polls; s_rec[5] = naps; s_rec[6] = uint32_t(n_items);
       uint4* out = reinterpret_cast<uint4*>(reinterpret_cast<char*>(P.v[0].ws) + parts_off(p.n_px)) + 2 * bid;
-      out[0] = make_uint4(rec[0], rec[1], rec[2], rec[3]);
-      out[1] = make_uint4(rec[4], rec[5], rec[6], rec[7]);
+      out[0] = make_uint4(s_rec[0], s_rec[1], s_rec[2], s_rec[3]);
+      out[1] = make_uint4(s_rec[4], s_rec[5], s_rec[6], s_rec[7]);
     }
   }
 }
@@ -2098,7 +2081,7 @@ int debug_flags() {   // profiling ablations only; unset in production
   return e ? atoi(e) : 0;
 }
 
-constexpr int kMainDbgBits = 1 | 2 | 4 | 8 | 64 | 128 | 256 | 512 | 0x3c00;   // 512: the instance alone   // bits main3's profiling instance reads
+constexpr int kMainDbgBits = 1 | 2 | 4 | 8 | 64 | 128 | 256 | 512;   // 512: the instance alone   // bits main3's profiling instance reads
 
 uint32_t help_after() {   // look-back helper delay; SLG_HELP_AFTER=0 forces the helper (tests)
   const char* e = getenv("SLG_HELP_AFTER");
