@@ -42,7 +42,7 @@ def worker(a):
     cal = rig.tables()
     dev = torch.device("cuda", 0)
     pool = [E.DeviceFrames(list(frames[i]), tex[i], device=dev) for _ in range(3) for i in range(12)]
-    dcal = E.DeviceCalib(cal, H, W, device=dev, tables=a.tables != "none")
+    dcal = E.DeviceCalib(cal, H, W, device=dev, tables=a.tables != "none", keep_table=a.tables == "rays")
     cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
     B = 12
     beng = E.BatchReconstructor(H, W, B, device=dev, slots=2)
@@ -89,7 +89,7 @@ def main():
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--worker", action="store_true")
-    ap.add_argument("--tables", default="num", help="worker: num | none (DeviceCalib numerator tables)")
+    ap.add_argument("--tables", default="num", help="worker: num | none (DeviceCalib numerator tables) | rays (also the Nc ray table)")
     ap.add_argument("--variants", default="", help="comma list of lib[:tables] (overrides --libs)")
     ap.add_argument("--timeout", type=int, default=240)
     a = ap.parse_args()
