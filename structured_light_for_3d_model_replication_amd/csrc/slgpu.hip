@@ -1765,20 +1765,10 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       if ((km[s][i] >> lane) & 1ull) {
         const int64_t q = base + s_loc[s][i][wave] + __popcll(km[s][i] & lt);
         const uint32_t c = s_bgr[bgr_slot(tid + kB * i)];
-        bool packed = false;
-        if constexpr (PROF && sizeof(XT) == 4) {     // PROF bit 8: one 16-byte {x, y, z, bgr} record
-          if (p.dbg & 256) {
-            if (q < p.n_px * 3 / 4)
-              reinterpret_cast<uint4*>(gx)[q] = make_uint4(__float_as_uint(float(pts[s][i][0])),
-                  __float_as_uint(float(pts[s][i][1])), __float_as_uint(float(pts[s][i][2])), c);
-            packed = true;
-          }
-        }
-        if (packed) {
-        } else if (!(PROF && (p.dbg & 128))) {       // PROF ablation bit 7: no XYZ stores
+        if (!(PROF && (p.dbg & 128))) {              // PROF ablation bit 7: no XYZ stores
           gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
         }
-        if (!packed && !(PROF && (p.dbg & 8))) {     // PROF ablation bit 3: no BGR stores
+        if (!(PROF && (p.dbg & 8))) {                // PROF ablation bit 3: no BGR stores
           gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
         }
       }
@@ -2081,7 +2071,7 @@ int debug_flags() {   // profiling ablations only; unset in production
   return e ? atoi(e) : 0;
 }
 
-constexpr int kMainDbgBits = 1 | 2 | 4 | 8 | 64 | 128 | 256 | 512;   // 512: the instance alone   // bits main3's profiling instance reads
+constexpr int kMainDbgBits = 1 | 2 | 4 | 8 | 64 | 128 | 512;   // 512: the instance alone   // bits main3's profiling instance reads
 
 uint32_t help_after() {   // look-back helper delay; SLG_HELP_AFTER=0 forces the helper (tests)
   const char* e = getenv("SLG_HELP_AFTER");
