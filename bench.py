@@ -494,7 +494,10 @@ def main():
                 "traffic": round(traffic_view * B) if traffic_view else None,
                 "traffic_source": "profiles/pmc_main_kernel.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"
                 if traffic_view else None,
-                "kernel": f"main3_kernel<1,{int(f64)},1,1> (fused decode+triangulate+compaction, {B} views per launch)",
+                "kernel": (f"main3_kernel<1,{int(f64)},1,1,false,PLAN=0x{(NC << 4) | NR:X}> (fused decode+triangulate+"
+                           f"compaction, decode-plan instance, {B} views per launch)"
+                           if (NC, NR) in ((11, 10), (11, 11), (12, 12)) else
+                           f"main3_kernel<1,{int(f64)},1,1> (fused decode+triangulate+compaction, {B} views per launch)"),
                 "kernel_avg_us": round(kern_avg_s * 1e6, 2),
                 "kernel_time": ("HIP events around each fused launch on its stream" if args.kernel_events == "launch"
                                 else "HIP events around the timed region (both launch streams joined) / steps: "
