@@ -9,8 +9,10 @@
 //                     them into integer mask thresholds (Otsu as OpenCV, or NumPy percentile);
 //                     also zeroes the compaction state of the next main launch.
 //   main3_kernel<...> fused decode + triangulate + ordered compaction, one 4096-pixel tile per
-//                     workgroup (512 lanes x 8 pixels), up to 16 views per launch: streams the
-//                     used frames with 8-byte-per-lane coalesced loads, SWAR byte compares,
+//                     workgroup (512 lanes x 8 pixels), up to 16 views per launch: the mask
+//                     first (white/black), then the used pattern frames only in lanes holding a
+//                     valid pixel, with 8-byte-per-lane coalesced loads (instances specialised on
+//                     the common decode plans issue them all unconditionally), SWAR byte compares,
 //                     packed 16-bit Gray->binary, wave-private LDS compaction of valid pixels,
 //                     fp64 ray-plane intersection, decoupled look-back over static tile ids,
 //                     compacted stores straight from registers; the grid's first workgroups
