@@ -23,6 +23,7 @@
  *   slg_reconstruct_batch  <- process_multi_ply(mode='batch') over view folders
  *                             (server/processing.py:314-334): many views, one stream
  *   slg_ply_write          <- ProcessingLogic._save_ply (server/processing.py:236-248), host side
+ *   slg_ply_format         <- the same lines formatted on the device (batch pipeline)
  *   slg_png_gray8_size /   <- cv2.imread(f, 0) of an 8-bit grayscale capture frame
  *   slg_png_gray8_decode      (server/processing.py:59-60,98-99), host side fast path
  *   slg_rays_match_pinhole <- the `Nc.shape[1] == h*w` ray source test
@@ -255,6 +256,17 @@ int32_t slg_gray_texture(const uint8_t *frame0, int64_t n_pixels, uint8_t *bgr, 
  * (<= 0: all cores).  Returns bytes written, or -SLG_ERR_* on failure. */
 int64_t slg_ply_write(const char *path, const double *xyz, const uint8_t *bgr, int64_t n,
                       int32_t n_threads);
+
+/* Device: the BODY of the same PLY (the lines after end_header), formatted on the GPU from a
+ * DEVICE cloud (xyz float64 [n][3], bgr uint8 [n][3]) into DEVICE `text`, so a batch's clouds
+ * leave HBM as the bytes to write (processing.py:245-248; byte-identical with slg_ply_write).
+ * `text` holds slg_ply_format_bound(n) bytes, `ws` slg_ply_format_ws_bytes(n) bytes (device).
+ * Asynchronous on `stream`; afterwards ws holds {int64 body_bytes; int32 bad; int32 pad}: bad
+ * != 0 means a coordinate is NaN, infinite or >= 9.2e14 in magnitude, the body is not written,
+ * and the caller formats on the host (slg_ply_write).  Returns 0 or SLG_ERR_*. */
+int64_t slg_ply_format_bound(int64_t n);
+int64_t slg_ply_format_ws_bytes(int64_t n);
+int32_t slg_ply_format(const double *xyz, const uint8_t *bgr, int64_t n, char *text, void *ws, void *stream);
 
 /* Host: frame ingest fast path for cv2.imread(f, 0) (processing.py:59-60,98-99) on 8-bit
  * grayscale, non-interlaced PNGs, where it is the identity on the stored samples.

@@ -100,6 +100,9 @@ EXPORTS = {
     "slg_decode_stats_partials_batch": (c_i32, [c_i32, c_i32, c_i32, ctypes.POINTER(DecodeParams), c_vp, c_i64,
                                                 c_vp]),
     "slg_ply_write": (c_i64, [ctypes.c_char_p, c_vp, c_vp, c_i64, c_i32]),
+    "slg_ply_format_bound": (c_i64, [c_i64]),
+    "slg_ply_format_ws_bytes": (c_i64, [c_i64]),
+    "slg_ply_format": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "slg_png_gray8_size": (c_i32, [ctypes.c_char_p, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
     "slg_png_gray8_decode": (c_i32, [ctypes.c_char_p, c_vp, c_i64, c_i32, c_i32]),
     "slg_rays_match_pinhole": (c_i32, [c_vp, c_i32, c_i32, c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_vp]),

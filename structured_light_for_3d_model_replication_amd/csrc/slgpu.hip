@@ -2346,6 +2346,165 @@ char* fmt_u8(unsigned v, char* p) {
   return p;
 }
 
+// ------------------------------------------------------------------ ASCII PLY on the device
+// The body of ProcessingLogic._save_ply (server/processing.py:245-248): one line per point,
+// f"{x:.4f} {y:.4f} {z:.4f} {r} {g} {b}\n", formatted by the GPU so the cloud never leaves HBM
+// as numbers and the host only writes bytes.  The same exact rounding as fmt4 (round(|x|*10^4)
+// on the exact binary value, ties to even, '-' from the sign bit); magnitudes >= 9.2e14 (the
+// host path prints those through glibc) raise the `bad` flag so the caller formats on the host.
+constexpr int kPlyBlock = 256;             // threads per workgroup
+constexpr int kPlyPts = 4;                 // consecutive points per thread
+constexpr int kPlyChunk = kPlyBlock * kPlyPts;
+constexpr int kPlyNumMax = 21;             // '-' + 15 integer digits + '.' + 4
+constexpr int kPlyLineMax = 3 * kPlyNumMax + 3 * 3 + 6;
+
+struct PlyWs {                              // device workspace header (include/slgpu.h)
+  int64_t total;                            // body bytes
+  int32_t bad;                              // a value the device cannot format exactly
+  int32_t pad;
+};
+
+// |x| * 10^4 rounded exactly; false when |x| >= 9.2e14, NaN or inf (handled by the caller)
+__device__ inline uint64_t fixed4(double x, bool& neg) {
+  const uint64_t bits = uint64_t(__double_as_longlong(x));
+  neg = bits >> 63;
+  const int bexp = int((bits >> 52) & 0x7ff);
+  uint64_t m = bits & ((uint64_t(1) << 52) - 1);
+  int e;
+  if (bexp == 0) { e = -1074; } else { m |= uint64_t(1) << 52; e = bexp - 1075; }
+  const unsigned __int128 v = (unsigned __int128)m * 10000u;   // < 2^67; e <= -3 below 9.2e14
+  const int k = -e;
+  if (k >= 127) return 0;
+  const unsigned __int128 q = v >> k;
+  const unsigned __int128 rem = v - (q << k);
+  const unsigned __int128 half = (unsigned __int128)1 << (k - 1);
+  return uint64_t(q) + ((rem > half || (rem == half && (uint64_t(q) & 1))) ? 1 : 0);
+}
+
+// the line of point i into o (kPlyLineMax bytes), its length; -1: not formattable here
+__device__ inline int ply_line(const double* xyz, const uint8_t* bgr, int64_t i, char* o) {
+  int len = 0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const double x = xyz[3 * i + c];
+    if (!(fabs(x) < 9.2e14)) return -1;          // NaN, inf, or beyond the exact fast path
+    bool neg;
+    const uint64_t n = fixed4(x, neg);
+    if (neg) o[len++] = '-';
+    uint64_t ip = n / 10000u;
+    const unsigned fr = unsigned(n - ip * 10000u);
+    char tmp[16];
+    int t = 0;
+    do { tmp[t++] = char('0' + ip % 10u); ip /= 10u; } while (ip);
+    while (t) o[len++] = tmp[--t];
+    o[len++] = '.';
+    o[len++] = char('0' + fr / 1000u);
+    o[len++] = char('0' + (fr / 100u) % 10u);
+    o[len++] = char('0' + (fr / 10u) % 10u);
+    o[len++] = char('0' + fr % 10u);
+    o[len++] = ' ';
+  }
+#pragma unroll
+  for (int c = 2; c >= 0; --c) {                 // BGR -> "R G B"
+    const unsigned v = bgr[3 * i + c];
+    if (v >= 100) o[len++] = char('0' + v / 100);
+    if (v >= 10) o[len++] = char('0' + (v / 10) % 10);
+    o[len++] = char('0' + v % 10);
+    o[len++] = c ? ' ' : '\n';
+  }
+  return len;
+}
+
+__device__ inline int ply_thread_bytes(const double* xyz, const uint8_t* bgr, int64_t n, int64_t i0, int* bad) {
+  char line[kPlyLineMax];
+  int sum = 0;
+  for (int j = 0; j < kPlyPts; ++j) {
+    const int64_t i = i0 + j;
+    if (i >= n) break;
+    const int l = ply_line(xyz, bgr, i, line);
+    if (l < 0) { atomicOr(bad, 1); return 0; }
+    sum += l;
+  }
+  return sum;
+}
+
+// Block-wide exclusive scan of one int per thread (kPlyBlock threads): (prefix, total).
+__device__ inline int2 ply_block_scan(int x, int* s_w) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kPlyBlock / 64; ++w) {
+    off += w < wave ? s_w[w] : 0;
+    tot += s_w[w];
+  }
+  return make_int2(off + incl - x, tot);
+}
+
+// pass 1: bytes per chunk
+__global__ __launch_bounds__(kPlyBlock) void ply_len_kernel(const double* xyz, const uint8_t* bgr, int64_t n,
+                                                           int64_t* chunk, PlyWs* hdr) {
+  __shared__ int s_w[kPlyBlock / 64];
+  const int64_t i0 = int64_t(blockIdx.x) * kPlyChunk + int64_t(threadIdx.x) * kPlyPts;
+  const int b = ply_thread_bytes(xyz, bgr, n, i0, &hdr->bad);
+  const int2 sc = ply_block_scan(b, s_w);
+  if (threadIdx.x == 0) chunk[blockIdx.x] = sc.y;
+}
+
+// pass 2: exclusive offsets of the chunks (one workgroup, serial over 1024-chunk strides)
+__global__ __launch_bounds__(1024) void ply_scan_kernel(int64_t* chunk, int64_t n_chunks, PlyWs* hdr) {
+  __shared__ int64_t s_w[16];
+  __shared__ int64_t s_carry;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n_chunks; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t x = i < n_chunks ? chunk[i] : 0;
+    int64_t incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    int64_t off = s_carry;
+    for (int w = 0; w < wave; ++w) off += s_w[w];
+    if (i < n_chunks) chunk[i] = off + incl - x;
+    __syncthreads();
+    if (threadIdx.x == 1023) s_carry = off + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) hdr->total = s_carry;
+}
+
+// pass 3: every thread writes its points' lines at the chunk offset + its prefix
+__global__ __launch_bounds__(kPlyBlock) void ply_write_kernel(const double* xyz, const uint8_t* bgr, int64_t n,
+                                                             const int64_t* chunk, char* text, PlyWs* hdr) {
+  __shared__ int s_w[kPlyBlock / 64];
+  if (hdr->bad) return;                                      // the caller formats on the host
+  const int64_t i0 = int64_t(blockIdx.x) * kPlyChunk + int64_t(threadIdx.x) * kPlyPts;
+  const int b = ply_thread_bytes(xyz, bgr, n, i0, &hdr->bad);
+  const int2 sc = ply_block_scan(b, s_w);
+  char* o = text + chunk[blockIdx.x] + sc.x;
+  char line[kPlyLineMax];
+  for (int j = 0; j < kPlyPts; ++j) {
+    const int64_t i = i0 + j;
+    if (i >= n) break;
+    const int l = ply_line(xyz, bgr, i, line);
+    for (int k = 0; k < l; ++k) o[k] = line[k];
+    o += l;
+  }
+}
+
 }  // namespace
 
 // Error entry for the library's other translation units (csrc/gather.cpp).
@@ -2463,6 +2622,32 @@ int32_t slg_reconstruct(const slg_capture* cap, const slg_decode_params* dp, con
 int32_t slg_decode_triangulate(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,
                                const slg_tri_params* tp, void* workspace, const slg_cloud* out, void* stream) {
   return reconstruct_impl(cap, dp, calib, tp, workspace, out, stream, false);
+}
+
+int64_t slg_ply_format_bound(int64_t n) { return n < 0 ? -fail(SLG_ERR_INVALID, "n < 0") : n * kPlyLineMax; }
+
+int64_t slg_ply_format_ws_bytes(int64_t n) {
+  if (n < 0) return -fail(SLG_ERR_INVALID, "n < 0");
+  return int64_t(sizeof(PlyWs)) + 8 * ((n + kPlyChunk - 1) / kPlyChunk + 1);
+}
+
+int32_t slg_ply_format(const double* xyz, const uint8_t* bgr, int64_t n, char* text, void* ws, void* stream) {
+  if (n < 0 || !ws || (n > 0 && (!xyz || !bgr || !text))) return fail(SLG_ERR_INVALID, "bad argument");
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  PlyWs* hdr = static_cast<PlyWs*>(ws);
+  int64_t* chunk = reinterpret_cast<int64_t*>(hdr + 1);
+  if (hipMemsetAsync(hdr, 0, sizeof(PlyWs), s) != hipSuccess) return fail(SLG_ERR_HIP, "hipMemsetAsync");
+  if (n == 0) return SLG_OK;
+  const int64_t nc = (n + kPlyChunk - 1) / kPlyChunk;
+  if (nc > INT_MAX) return fail(SLG_ERR_UNSUPPORTED, "cloud too large");
+  hipLaunchKernelGGL(ply_len_kernel, dim3(unsigned(nc)), dim3(kPlyBlock), 0, s, xyz, bgr, n, chunk, hdr);
+  int rc = check_launch("ply_len_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ply_scan_kernel, dim3(1), dim3(1024), 0, s, chunk, nc, hdr);
+  rc = check_launch("ply_scan_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ply_write_kernel, dim3(unsigned(nc)), dim3(kPlyBlock), 0, s, xyz, bgr, n, chunk, text, hdr);
+  return check_launch("ply_write_kernel");
 }
 
 int64_t slg_ply_write(const char* path, const double* xyz, const uint8_t* bgr, int64_t n, int32_t n_threads) {

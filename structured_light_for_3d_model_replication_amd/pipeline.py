@@ -12,8 +12,11 @@ write an ASCII PLY.  Here the same work is a pipeline whose stages overlap:
   colour upload), then ONE batched stats launch + ONE fused decode/triangulate launch for the
   group (``BatchReconstructor.run``, ``slg_reconstruct_batch``) -- launched before the previous
   group is collected, so uploads and kernels of consecutive groups overlap;
-* **collect**: counts, D2H of the float64 clouds into pinned buffers;
-* **write** (writer thread): ``slg_ply_write`` (byte-identical ASCII PLY).
+* **collect**: counts; each view's PLY body formatted on the device (``slg_ply_format``, on a
+  stream of its own beside the next group's kernels) and copied into pinned host memory as
+  bytes (a cloud with a value the device formatter leaves to the host: its float64 points);
+* **write** (writer thread): header + body (byte-identical ASCII PLY; ``slg_ply_write`` for
+  host clouds).
 
 Per-folder behaviour is the reference's: folders without images are skipped with its message,
 an exception in any stage of one folder is logged as ``❌ Error in <folder>: <msg>`` and the loop
@@ -36,6 +39,7 @@ import torch
 from . import _native as N
 from . import engine as E
 from . import frames as FR
+from . import ply as PLY
 
 
 class PinnedPool:
@@ -179,6 +183,26 @@ def upload_view(hv: HostView, stream, need=None) -> E.DeviceFrames:
 
 
 @dataclass
+class FormattedCloud:
+    """A view's PLY body formatted on the device (``slg_ply_format``), in pinned host memory."""
+    n_points: int
+    body: torch.Tensor              # pinned uint8, the first `length` bytes are the body
+    length: int
+    pool: PinnedPool
+
+    def write(self, filename) -> None:
+        try:
+            PLY.write_body(filename, self.n_points, self.body[: self.length].numpy())
+        finally:
+            self.pool.put(self.body)
+
+
+def n_points(result) -> int:
+    """Points of a collected view: a FormattedCloud or a host (P, C) pair."""
+    return result.n_points if isinstance(result, FormattedCloud) else len(result[0])
+
+
+@dataclass
 class _Group:
     entries: list                   # [(folder, future | None)] in folder order (None: skipped)
     views: list = field(default_factory=list)   # [(index in entries, HostView, DeviceFrames)]
@@ -192,7 +216,7 @@ class BatchPipeline:
     """The pipeline of this module's docstring for one decode configuration + calibration."""
 
     def __init__(self, cfg: E.DecodeConfig, calib: dict, row_mode=1, epipolar_tol=2.0, group: int = 8,
-                 depth: int | None = None, log=print, order=("bmp", "png")):
+                 depth: int | None = None, log=print, order=("bmp", "png"), device_ply: bool = True):
         if row_mode not in (0, 1, 2):
             raise ValueError("row_mode must be 0, 1 or 2")
         self.cfg, self.calib, self.row_mode, self.tol = cfg, calib, int(row_mode), float(epipolar_tol)
@@ -202,6 +226,9 @@ class BatchPipeline:
         self.pool = PinnedPool()
         self.copy_stream = torch.cuda.Stream()
         self.compute_stream = torch.cuda.Stream()
+        self.format_stream = torch.cuda.Stream()     # PLY bodies of group k beside group k+1's kernels
+        self.formatter = PLY.DeviceFormatter()
+        self.device_ply = device_ply
         self.engines: dict = {}
         self.tables: dict = {}
         self._slot = 0
@@ -256,7 +283,13 @@ class BatchPipeline:
         if g.batch is not None:
             for (k, hv, _), c in zip(g.views, g.clouds):
                 n = int(c.count.item())
-                res[k] = (c.xyz[:n].cpu().numpy(), c.bgr[:n].cpu().numpy())
+                body = self.formatter.body(c.xyz[:n], c.bgr[:n], self.format_stream) if self.device_ply else None
+                if body is None:                        # host formatting (or a value it must print)
+                    res[k] = (c.xyz[:n].cpu().numpy(), c.bgr[:n].cpu().numpy())
+                else:                                   # the PLY body leaves HBM as bytes
+                    host = self.pool.get((body.numel() + (16 << 20) - 1) // (16 << 20) * (16 << 20))
+                    host[: body.numel()].copy_(body)
+                    res[k] = FormattedCloud(n, host, body.numel(), self.pool)
         else:                                       # isolate the failing view(s)
             from .processing import reconstruct_view
             for k, hv, dev in g.views:
@@ -336,7 +369,7 @@ class BatchPipeline:
             r, wf, err = outcome[k]
             if err is None:
                 log("  -> Reconstructing 3D points...")
-                log(f"  -> Saving {len(r[0])} points...")
+                log(f"  -> Saving {n_points(r)} points...")
                 try:
                     out = wf.result()
                     ok += 1

@@ -361,9 +361,14 @@ def batch_reconstruct_stage(cfg, calib, row_mode, epipolar_tol, log):
 
 def batch_write_stage():
     """``write`` stage of :func:`run_view_folders`: ``<folder>/<folder name>.ply``."""
+    from .pipeline import FormattedCloud
+
     def stage(folder, result):
         name = os.path.basename(folder) + ".ply"
-        ProcessingLogic._save_ply(result[0], result[1], os.path.join(folder, name))
+        if isinstance(result, FormattedCloud):          # body formatted on the device
+            result.write(os.path.join(folder, name))
+        else:
+            ProcessingLogic._save_ply(result[0], result[1], os.path.join(folder, name))
         return name
     return stage
 
