@@ -49,7 +49,8 @@ class DeviceFormatter:
     def body(self, xyz, bgr, stream=None):
         """Body bytes of the PLY of a device cloud (xyz float64 [n, 3], bgr uint8 [n, 3]) as a
         DEVICE uint8 tensor view, or None when a coordinate needs the host formatter (NaN, inf,
-        |x| >= 9.2e14).  Synchronises ``stream`` to read the length."""
+        |x| >= 9.2e14).  Synchronises ``stream`` to read the length.  The view aliases this
+        formatter's buffer: copy it out before the next call."""
         import ctypes
         import torch
         from . import _native as N
