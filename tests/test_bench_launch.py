@@ -57,3 +57,22 @@ def test_spawn_ranks_propagates_failure(tmp_path):
     script = tmp_path / "fail.py"
     script.write_text("import os, sys\nsys.exit(3 if os.environ['RANK'] == '1' else 0)\n")
     assert bench.spawn_ranks(2, [], script=str(script)) == 3
+
+
+def test_mask_first_segments_count():
+    """bench.segments_holding (the mask-first algorithmic bytes): 64-byte segments of each frame
+    that hold a valid pixel, checked against a brute-force count, with frames at offsets that
+    are and are not multiples of 64."""
+    import numpy as np
+    import torch
+    rng = np.random.default_rng(5)
+    n_px = 5000
+    mask = rng.random(n_px) < 0.05
+    mask[:70] = True                                   # a run across a segment boundary
+    for stride, frames in ((5056, [0, 2, 3]), (5008, [0, 1, 2, 5])):
+        want = 0
+        for f in frames:
+            segs = set(((f * stride + np.nonzero(mask)[0]) >> 6).tolist())
+            want += len(segs)
+        assert bench.segments_holding(torch.from_numpy(mask), stride, frames) == want
+    assert bench.segments_holding(torch.zeros(n_px, dtype=torch.bool), 5056, [0, 1]) == 0
