@@ -760,7 +760,8 @@ struct NoPre {
 };
 
 // PLAN: (col_pairs << 4) | row_pairs as compile-time constants (main3's specialised instances for
-// the common capture layouts, kPlans), or 0: the counts come from the view's plan at run time.
+// the common capture layouts, SLG_PLAN_*; every view of such a launch has that plan), or 0: the
+// counts come from the view's plan at run time.
 // Constant counts make every frame load unconditional, so the decode consumes each pair as it
 // lands (vmcnt(n) in issue order) instead of after a vmcnt(0) for the whole batch, and drop the
 // per-pair branches (243.3 vs 259.8 us per 12-view launch, profiles/r3m).
