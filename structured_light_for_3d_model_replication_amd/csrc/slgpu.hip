@@ -160,6 +160,10 @@ constexpr int kStatsBlocks = 64;            // stats workgroups per view (at mos
 #define SLG_STATS_OTSU_BLOCKS 64                 // 128: 2.6% and 256: 10% slower bench (slot contention)
 #endif
 constexpr int kStatsBlocksOtsu = SLG_STATS_OTSU_BLOCKS;   // matrix-core Otsu path
+#ifndef SLG_STATS_BLOCKS_SOLO
+#define SLG_STATS_BLOCKS_SOLO 256   // r3ao: 64 -> 51.7, 128 -> 42.2, 256 -> 40.0, 512 -> 39.9 us (1080p, Otsu)
+#endif
+constexpr int kStatsBlocksSolo = SLG_STATS_BLOCKS_SOLO;   // one-view launches (nothing runs beside them)
 
 struct StatsParams {
   const uint8_t* white[kMaxBatch];
@@ -245,18 +249,46 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
       yr[j] = 1.0 / q1r[j];
     }
   }
-  const int l_end = 64 - __builtin_clzll(__ballot(okr != 0) | 1ull);   // lanes with work: [0, l_end)
-  double mu1 = 0.0;                                  // 3. the mu1 chain
-  for (int l = 0; l < l_end; ++l) {
-    const uint32_t okl = __builtin_amdgcn_readlane(okr, l);
+  // 3. the mu1 chain.  The unskipped bins form one run [lo, hi]: q1 never decreases and
+  // q2 = RN(1 - q1) never increases, so each skip test holds on a prefix plus a suffix of the
+  // bins, and mu1 is still 0 at lo.  Over the run every bin is the same 7 dependent ops with no
+  // per-bin test when every numerator suits div_rn: a is 0, or at least ~1/n (an empty bin's
+  // mu1 *= q1 then / q1 moves a by ulps), so n <= 2^52 keeps a far inside its range.  Anything
+  // else (never seen) takes the general loop: per-bin skip flags, IEEE division when refused.
+  const uint64_t lanes_ok = __ballot(okr != 0);
+  int lo = 256, hi = -1, n_ok = 0;
+  if (lanes_ok) {
+    const int l_lo = __builtin_ctzll(lanes_ok), l_hi = 63 - __builtin_clzll(lanes_ok);
+    lo = 4 * l_lo + __builtin_ctz(__builtin_amdgcn_readlane(okr, l_lo));
+    hi = 4 * l_hi + 31 - __builtin_clz(__builtin_amdgcn_readlane(okr, l_hi));
+  }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      mu1 *= readlane_f64(qpr[j], l);                // mu1 *= q1 (previous q1)
-      if (okl & (1u << j)) {
-        const double a = mu1 + readlane_f64(ip[j], l);
-        const double q = readlane_f64(q1r[j], l);
-        mu1 = div_rn_ok(a) ? div_rn(a, q, readlane_f64(yr[j], l)) : a / q;
+  for (int j = 0; j < 4; ++j) n_ok += __popcll(__ballot((okr >> j) & 1u));
+  double mu1 = 0.0;
+  if (n_ok == hi - lo + 1 && n <= (int64_t(1) << 52)) {
+    for (int l = lo >> 2; l <= (hi >> 2); ++l) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * l + j;
+        if (i < lo || i > hi) continue;              // scalar: first and last lane only
+        const double a = mu1 * readlane_f64(qpr[j], l) + readlane_f64(ip[j], l);
+        mu1 = div_rn(a, readlane_f64(q1r[j], l), readlane_f64(yr[j], l));
         if (lane == l) m1r[j] = mu1;
+      }
+    }
+  } else {
+    const int l_end = 64 - __builtin_clzll(lanes_ok | 1ull);   // lanes with work: [0, l_end)
+    for (int l = 0; l < l_end; ++l) {
+      const uint32_t okl = __builtin_amdgcn_readlane(okr, l);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mu1 *= readlane_f64(qpr[j], l);              // mu1 *= q1 (previous q1)
+        if (okl & (1u << j)) {
+          const double a = mu1 + readlane_f64(ip[j], l);
+          const double q = readlane_f64(q1r[j], l);
+          mu1 = div_rn_ok(a) ? div_rn(a, q, readlane_f64(yr[j], l)) : a / q;
+          if (lane == l) m1r[j] = mu1;
+        }
       }
     }
   }
@@ -1237,12 +1269,15 @@ __device__ bool lookback_scalar(const MainParams& p, uint64_t* st, int tile, int
 }
 
 // Correspondence maps of 2048 pixels per workgroup (slg_decode): col/row int32, mask uint8.
+// PLAN: as main3's decode-plan instances (every load of the capture issued unconditionally, in
+// one batch of 11 pairs per axis); 0: the plan's counts at run time, 8 pairs per batch.
+template <int PLAN>
 __global__ __launch_bounds__(kBlock) void decode_maps_kernel(MainParams p) {
   const int64_t px0 = int64_t(blockIdx.x) * kMapsPx + int64_t(threadIdx.x) * kPx;
   const bool tail = px0 + kPx > p.n_px;       // lane-level guard for the ragged end
   uint32_t valid;
   int col[kPx], row[kPx];
-  decode_lane<1, 1, 8>(p, px0, tail, valid, col, row);
+  decode_lane<1, 1, PLAN ? 11 : 8, false, PLAN>(p, px0, tail, valid, col, row);
   if (px0 + kPx <= p.n_px) {
     int4* oc = reinterpret_cast<int4*>(p.out_col + px0);
     int4* orr = reinterpret_cast<int4*>(p.out_row + px0);
@@ -1982,7 +2017,8 @@ int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* black
   // Few fat workgroups per view: each merges its sub-histograms into the view's histogram with
   // <= 512 global atomics, and a batch's stats pass takes few CU slots next to a fused launch.
   int64_t grid = (n_px + int64_t(kBlock) * kStatsPx - 1) / (int64_t(kBlock) * kStatsPx);
-  const int64_t cap = sp.thresh_mode == SLG_THRESH_OTSU ? kStatsBlocksOtsu : kStatsBlocks;
+  const int64_t cap = n_views == 1 ? kStatsBlocksSolo
+                    : sp.thresh_mode == SLG_THRESH_OTSU ? kStatsBlocksOtsu : kStatsBlocks;
   if (grid > cap) grid = cap;
   if (sp.thresh_mode == SLG_THRESH_OTSU) {   // bound chunks per wave (i32 MFMA accumulators)
     const int64_t per_block = int64_t(kBlock / 64) * kHistChunk * kHistMaxChunks;
@@ -2568,7 +2604,11 @@ int32_t slg_decode(const slg_capture* cap, const slg_decode_params* dp, void* wo
   mp.out_col = col_out; mp.out_row = row_out; mp.out_mask = mask_out;
   mp.ws = reinterpret_cast<WsHeader*>(workspace);
   mp.n_tiles = n_tiles_of(n_px);
-  hipLaunchKernelGGL(decode_maps_kernel, dim3(unsigned((n_px + kMapsPx - 1) / kMapsPx)), dim3(kBlock), 0,
+  const int key = pl.col_pairs <= 15 && pl.row_pairs <= 15 ? (pl.col_pairs << 4) | pl.row_pairs : 0;
+  void (*fn)(MainParams) = key == SLG_PLAN_C2 ? decode_maps_kernel<SLG_PLAN_C2>
+                         : key == SLG_PLAN_1080P ? decode_maps_kernel<SLG_PLAN_1080P>
+                         : key == SLG_PLAN_C4 ? decode_maps_kernel<SLG_PLAN_C4> : decode_maps_kernel<0>;
+  hipLaunchKernelGGL(fn, dim3(unsigned((n_px + kMapsPx - 1) / kMapsPx)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), mp);
   return check_launch("decode_maps_kernel");
 }

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--size", default="1920x1080")
     ap.add_argument("--views", type=int, default=12)
     ap.add_argument("--only", default="")
+    ap.add_argument("--thresh", default="otsu", choices=("otsu", "percentile"))
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -39,7 +40,7 @@ def main():
     dfr = [E.DeviceFrames(list(v.frames), v.texture) for v in views]
     dcal = E.DeviceCalib(cal, H, W)
     eng = E.Reconstructor(H, W)
-    cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
+    cfg = E.DecodeConfig(1920, 1080, 11, 10, args.thresh)
     s = torch.cuda.current_stream()
     clouds = {rm: E.Cloud(H * W, rm, False) for rm in (0, 1, 2)}
     maps = [eng.decode(d, cfg) for d in dfr]
