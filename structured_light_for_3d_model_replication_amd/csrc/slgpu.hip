@@ -160,6 +160,9 @@ constexpr int kStatsBlocks = 64;            // stats workgroups per view (at mos
 #define SLG_STATS_OTSU_BLOCKS 64                 // 128: 2.6% and 256: 10% slower bench (slot contention)
 #endif
 constexpr int kStatsBlocksOtsu = SLG_STATS_OTSU_BLOCKS;   // matrix-core Otsu path
+#ifndef SLG_STATS_ABL
+#define SLG_STATS_ABL 0   // profiling ablations (tools/gpu_r3aq.sh): 1 no MFMA, 2 no merge, 4 no mu1 run, 8 no q1 chain
+#endif
 #ifndef SLG_STATS_BLOCKS_SOLO
 #define SLG_STATS_BLOCKS_SOLO 256   // r3ao: 64 -> 51.7, 128 -> 42.2, 256 -> 40.0, 512 -> 39.9 us (1080p, Otsu)
 #endif
@@ -232,7 +235,7 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
   isum = wave_sum(isum);
   const double mu = double(isum) * scale;
   double q1 = 0.0;                                   // 1. the q1 chain (OpenCV's order)
-  for (int l = 0; l < 64; ++l) {
+  for (int l = 0; l < ((SLG_STATS_ABL & 8) ? 1 : 64); ++l) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const double nq = q1 + readlane_f64(pv[j], l);
@@ -266,7 +269,7 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
   for (int j = 0; j < 4; ++j) n_ok += __popcll(__ballot((okr >> j) & 1u));
   double mu1 = 0.0;
   if (n_ok == hi - lo + 1 && n <= (int64_t(1) << 52)) {
-    for (int l = lo >> 2; l <= (hi >> 2); ++l) {
+    for (int l = lo >> 2; l <= ((SLG_STATS_ABL & 4) ? (lo >> 2) : (hi >> 2)); ++l) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int i = 4 * l + j;
@@ -465,7 +468,11 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
       uint32_t wn[4], dn[4];
       const bool more = c + step < p.n_px;
       if (more) hist_load(white, black, c + step, p.n_px, wn, dn);
+#if SLG_STATS_ABL & 1
+      acc_w[0] += int(w[0] ^ d[1]);
+#else
       mfma_hist_chunk(s_stage + wave * 256, w, d, acc_w, acc_d);
+#endif
       if (more) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) { w[q] = wn[q]; d[q] = dn[q]; }
@@ -510,7 +517,12 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
     uint32_t v = 0;
 #pragma unroll
     for (int c = 0; c < 16; ++c) v += sh[(2 * c + kind) * kRow + bin];
-    if (v) atomicAdd(hist_part + (blockIdx.x % kHistCopies) * 512 + i, v);
+#if SLG_STATS_ABL & 2
+    if (v == 0xffffffffu)
+#else
+    if (v)
+#endif
+      atomicAdd(hist_part + (blockIdx.x % kHistCopies) * 512 + i, v);
   }
   if (!otsu && tid == 0 && s_maxd) atomicMax(&ws->max_diff_enc, s_maxd);
 
