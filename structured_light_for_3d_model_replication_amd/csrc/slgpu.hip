@@ -161,12 +161,16 @@ constexpr int kStatsBlocks = 64;            // stats workgroups per view (at mos
 #endif
 constexpr int kStatsBlocksOtsu = SLG_STATS_OTSU_BLOCKS;   // matrix-core Otsu path
 #ifndef SLG_STATS_ABL
-#define SLG_STATS_ABL 0   // profiling ablations (tools/gpu_r3aq.sh): 1 no MFMA, 2 no merge, 4 no mu1 run, 8 no q1 chain
+#define SLG_STATS_ABL 0   // profiling ablations (tools/gpu_r3aq.sh): 1 no MFMA, 2 no merge
 #endif
 #ifndef SLG_STATS_BLOCKS_SOLO
 #define SLG_STATS_BLOCKS_SOLO 256   // r3ao: 64 -> 51.7, 128 -> 42.2, 256 -> 40.0, 512 -> 39.9 us (1080p, Otsu)
 #endif
 constexpr int kStatsBlocksSolo = SLG_STATS_BLOCKS_SOLO;   // one-view launches (nothing runs beside them)
+#ifndef SLG_OTSU_SOLO_CHUNKS
+#define SLG_OTSU_SOLO_CHUNKS 2
+#endif
+constexpr int kOtsuSoloChunks = SLG_OTSU_SOLO_CHUNKS;
 
 struct StatsParams {
   const uint8_t* white[kMaxBatch];
@@ -218,11 +222,54 @@ __device__ inline double readlane_f64(double v, int l) {
   return __longlong_as_double((long long)((uint64_t(hi) << 32) | lo));
 }
 
+// otsu_wave's mu1 run over bins [lo, hi].  SPEC: each quotient as fma(a, y, a * y_lo), where
+// y + y_lo = 1/q1 to ~2^-105 (1 - q1 y is exact; y_lo off the chain): 2 dependent ops instead
+// of div_rn's 5.  The result is faithful, and
+// RN(a / q1) unless a / q1 sits within ~2^-105 of a rounding boundary, so the caller checks every
+// bin afterwards (Markstein: RN(m + (a - q1 m) y) = RN(a / q1) for faithful m) and reruns
+// without SPEC on a miss.  ar keeps each bin's numerator for that check.
+template <bool SPEC, int J>
+__device__ inline void mu1_bin(int l, double& mu1, double& q_prev, const double (&ip)[4], const double (&q1r)[4],
+                               const double (&yr)[4], double (&m1r)[4], double (&ar)[4]) {
+  const double a = mu1 * q_prev + readlane_f64(ip[J], l);
+  q_prev = readlane_f64(q1r[J], l);
+  const double y = readlane_f64(yr[J], l);
+  if (SPEC)
+    mu1 = fma(a, y, a * (fma(-q_prev, y, 1.0) * y));
+  else
+    mu1 = div_rn(a, q_prev, y);
+  if ((threadIdx.x & 63) == l) {
+    m1r[J] = mu1;
+    if (SPEC) ar[J] = a;
+  }
+}
+
+template <bool SPEC>
+__device__ inline void mu1_run(int lo, int hi, const double (&ip)[4], const double (&q1r)[4], const double (&yr)[4],
+                               double (&m1r)[4], double (&ar)[4]) {
+  double mu1 = 0.0, q_prev = 0.0;                    // bin i's previous q1 is bin i-1's q1 (mu1 = 0 at lo)
+  const int l0 = lo >> 2, l1 = hi >> 2;
+  auto edge = [&](int l) {                           // the run's first and last lane: bin by bin
+    if (4 * l + 0 >= lo && 4 * l + 0 <= hi) mu1_bin<SPEC, 0>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
+    if (4 * l + 1 >= lo && 4 * l + 1 <= hi) mu1_bin<SPEC, 1>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
+    if (4 * l + 2 >= lo && 4 * l + 2 <= hi) mu1_bin<SPEC, 2>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
+    if (4 * l + 3 >= lo && 4 * l + 3 <= hi) mu1_bin<SPEC, 3>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
+  };
+  edge(l0);
+  for (int l = l0 + 1; l < l1; ++l) {                // interior lanes: 4 bins, no tests
+    mu1_bin<SPEC, 0>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
+    mu1_bin<SPEC, 1>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
+    mu1_bin<SPEC, 2>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
+    mu1_bin<SPEC, 3>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
+  }
+  if (l1 > l0) edge(l1);
+}
+
 __device__ double otsu_wave(const uint32_t* h, int64_t n) {
   const int lane = threadIdx.x & 63;
   const double scale = 1.0 / double(n);
   const double eps = double(__FLT_EPSILON__);
-  double pv[4], ip[4], q1r[4], qpr[4], yr[4], m1r[4];
+  double pv[4], ip[4], q1r[4], yr[4], m1r[4], ar[4];
   uint64_t isum = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -230,16 +277,16 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
     pv[j] = double(h[i]) * scale;
     ip[j] = double(i) * pv[j];
     isum += uint64_t(i) * h[i];
-    q1r[j] = qpr[j] = yr[j] = m1r[j] = 0.0;
+    q1r[j] = yr[j] = m1r[j] = ar[j] = 0.0;
   }
   isum = wave_sum(isum);
   const double mu = double(isum) * scale;
   double q1 = 0.0;                                   // 1. the q1 chain (OpenCV's order)
-  for (int l = 0; l < ((SLG_STATS_ABL & 8) ? 1 : 64); ++l) {
+  for (int l = 0; l < 64; ++l) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const double nq = q1 + readlane_f64(pv[j], l);
-      if (lane == l) { qpr[j] = q1; q1r[j] = nq; }
+      if (lane == l) q1r[j] = nq;
       q1 = nq;
     }
   }
@@ -254,10 +301,11 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
   }
   // 3. the mu1 chain.  The unskipped bins form one run [lo, hi]: q1 never decreases and
   // q2 = RN(1 - q1) never increases, so each skip test holds on a prefix plus a suffix of the
-  // bins, and mu1 is still 0 at lo.  Over the run every bin is the same 7 dependent ops with no
-  // per-bin test when every numerator suits div_rn: a is 0, or at least ~1/n (an empty bin's
-  // mu1 *= q1 then / q1 moves a by ulps), so n <= 2^52 keeps a far inside its range.  Anything
-  // else (never seen) takes the general loop: per-bin skip flags, IEEE division when refused.
+  // bins, and mu1 is still 0 at lo.  Over the run every bin is the same 4 dependent ops
+  // (mu1_run<true>, checked afterwards; 7 in mu1_run<false>) with no per-bin test when every
+  // numerator suits div_rn: a is 0, or at least ~1/n (an empty bin's mu1 *= q1 then / q1 moves
+  // a by ulps), so n <= 2^52 keeps a far inside its range.  Anything else (never seen) takes the
+  // general loop: per-bin skip flags, IEEE division when refused.
   const uint64_t lanes_ok = __ballot(okr != 0);
   int lo = 256, hi = -1, n_ok = 0;
   if (lanes_ok) {
@@ -269,29 +317,29 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
   for (int j = 0; j < 4; ++j) n_ok += __popcll(__ballot((okr >> j) & 1u));
   double mu1 = 0.0;
   if (n_ok == hi - lo + 1 && n <= (int64_t(1) << 52)) {
-    for (int l = lo >> 2; l <= ((SLG_STATS_ABL & 4) ? (lo >> 2) : (hi >> 2)); ++l) {
+    mu1_run<true>(lo, hi, ip, q1r, yr, m1r, ar);
+    uint32_t miss = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int i = 4 * l + j;
-        if (i < lo || i > hi) continue;              // scalar: first and last lane only
-        const double a = mu1 * readlane_f64(qpr[j], l) + readlane_f64(ip[j], l);
-        mu1 = div_rn(a, readlane_f64(q1r[j], l), readlane_f64(yr[j], l));
-        if (lane == l) m1r[j] = mu1;
-      }
+    for (int j = 0; j < 4; ++j) {
+      const double r = fma(-q1r[j], m1r[j], ar[j]);   // exact remainder
+      if ((okr >> j) & 1u) miss |= uint32_t(fma(r, yr[j], m1r[j]) != m1r[j]);
     }
+    if (__ballot(miss != 0)) mu1_run<false>(lo, hi, ip, q1r, yr, m1r, ar);
   } else {
     const int l_end = 64 - __builtin_clzll(lanes_ok | 1ull);   // lanes with work: [0, l_end)
+    double q_prev = 0.0;
     for (int l = 0; l < l_end; ++l) {
       const uint32_t okl = __builtin_amdgcn_readlane(okr, l);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        mu1 *= readlane_f64(qpr[j], l);              // mu1 *= q1 (previous q1)
+        mu1 *= q_prev;                               // mu1 *= q1 (previous q1)
+        const double q = readlane_f64(q1r[j], l);
         if (okl & (1u << j)) {
           const double a = mu1 + readlane_f64(ip[j], l);
-          const double q = readlane_f64(q1r[j], l);
           mu1 = div_rn_ok(a) ? div_rn(a, q, readlane_f64(yr[j], l)) : a / q;
           if (lane == l) m1r[j] = mu1;
         }
+        q_prev = q;
       }
     }
   }
@@ -1281,15 +1329,13 @@ __device__ bool lookback_scalar(const MainParams& p, uint64_t* st, int tile, int
 }
 
 // Correspondence maps of 2048 pixels per workgroup (slg_decode): col/row int32, mask uint8.
-// PLAN: as main3's decode-plan instances (every load of the capture issued unconditionally, in
-// one batch of 11 pairs per axis); 0: the plan's counts at run time, 8 pairs per batch.
-template <int PLAN>
+// (Plan-specialised instances as main3's measured the same: 21.3 vs 21.4 us at 1080p, r3an2.)
 __global__ __launch_bounds__(kBlock) void decode_maps_kernel(MainParams p) {
   const int64_t px0 = int64_t(blockIdx.x) * kMapsPx + int64_t(threadIdx.x) * kPx;
   const bool tail = px0 + kPx > p.n_px;       // lane-level guard for the ragged end
   uint32_t valid;
   int col[kPx], row[kPx];
-  decode_lane<1, 1, PLAN ? 11 : 8, false, PLAN>(p, px0, tail, valid, col, row);
+  decode_lane<1, 1, 8>(p, px0, tail, valid, col, row);
   if (px0 + kPx <= p.n_px) {
     int4* oc = reinterpret_cast<int4*>(p.out_col + px0);
     int4* orr = reinterpret_cast<int4*>(p.out_row + px0);
@@ -2028,8 +2074,11 @@ int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* black
   sp.dbg = debug_flags();
   // Few fat workgroups per view: each merges its sub-histograms into the view's histogram with
   // <= 512 global atomics, and a batch's stats pass takes few CU slots next to a fused launch.
-  int64_t grid = (n_px + int64_t(kBlock) * kStatsPx - 1) / (int64_t(kBlock) * kStatsPx);
-  const int64_t cap = n_views == 1 ? kStatsBlocksSolo
+  // One-view Otsu launches: kOtsuSoloChunks MFMA chunks per wave.
+  const bool otsu_solo = n_views == 1 && sp.thresh_mode == SLG_THRESH_OTSU;
+  const int64_t px_per_block = otsu_solo ? int64_t(kBlock / 64) * kHistChunk * kOtsuSoloChunks : int64_t(kBlock) * kStatsPx;
+  int64_t grid = (n_px + px_per_block - 1) / px_per_block;
+  const int64_t cap = otsu_solo ? 4 * kStatsBlocksSolo : n_views == 1 ? kStatsBlocksSolo
                     : sp.thresh_mode == SLG_THRESH_OTSU ? kStatsBlocksOtsu : kStatsBlocks;
   if (grid > cap) grid = cap;
   if (sp.thresh_mode == SLG_THRESH_OTSU) {   // bound chunks per wave (i32 MFMA accumulators)
@@ -2616,11 +2665,7 @@ int32_t slg_decode(const slg_capture* cap, const slg_decode_params* dp, void* wo
   mp.out_col = col_out; mp.out_row = row_out; mp.out_mask = mask_out;
   mp.ws = reinterpret_cast<WsHeader*>(workspace);
   mp.n_tiles = n_tiles_of(n_px);
-  const int key = pl.col_pairs <= 15 && pl.row_pairs <= 15 ? (pl.col_pairs << 4) | pl.row_pairs : 0;
-  void (*fn)(MainParams) = key == SLG_PLAN_C2 ? decode_maps_kernel<SLG_PLAN_C2>
-                         : key == SLG_PLAN_1080P ? decode_maps_kernel<SLG_PLAN_1080P>
-                         : key == SLG_PLAN_C4 ? decode_maps_kernel<SLG_PLAN_C4> : decode_maps_kernel<0>;
-  hipLaunchKernelGGL(fn, dim3(unsigned((n_px + kMapsPx - 1) / kMapsPx)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(decode_maps_kernel, dim3(unsigned((n_px + kMapsPx - 1) / kMapsPx)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), mp);
   return check_launch("decode_maps_kernel");
 }
