@@ -228,41 +228,29 @@ __device__ inline double readlane_f64(double v, int l) {
 // RN(a / q1) unless a / q1 sits within ~2^-105 of a rounding boundary, so the caller checks every
 // bin afterwards (Markstein: RN(m + (a - q1 m) y) = RN(a / q1) for faithful m) and reruns
 // without SPEC on a miss.  ar keeps each bin's numerator for that check.
-template <bool SPEC, int J>
-__device__ inline void mu1_bin(int l, double& mu1, double& q_prev, const double (&ip)[4], const double (&q1r)[4],
-                               const double (&yr)[4], double (&m1r)[4], double (&ar)[4]) {
-  const double a = mu1 * q_prev + readlane_f64(ip[J], l);
-  q_prev = readlane_f64(q1r[J], l);
-  const double y = readlane_f64(yr[J], l);
-  if (SPEC)
-    mu1 = fma(a, y, a * (fma(-q_prev, y, 1.0) * y));
-  else
-    mu1 = div_rn(a, q_prev, y);
-  if ((threadIdx.x & 63) == l) {
-    m1r[J] = mu1;
-    if (SPEC) ar[J] = a;
-  }
-}
-
 template <bool SPEC>
 __device__ inline void mu1_run(int lo, int hi, const double (&ip)[4], const double (&q1r)[4], const double (&yr)[4],
                                double (&m1r)[4], double (&ar)[4]) {
+  const int lane = threadIdx.x & 63;
   double mu1 = 0.0, q_prev = 0.0;                    // bin i's previous q1 is bin i-1's q1 (mu1 = 0 at lo)
-  const int l0 = lo >> 2, l1 = hi >> 2;
-  auto edge = [&](int l) {                           // the run's first and last lane: bin by bin
-    if (4 * l + 0 >= lo && 4 * l + 0 <= hi) mu1_bin<SPEC, 0>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
-    if (4 * l + 1 >= lo && 4 * l + 1 <= hi) mu1_bin<SPEC, 1>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
-    if (4 * l + 2 >= lo && 4 * l + 2 <= hi) mu1_bin<SPEC, 2>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
-    if (4 * l + 3 >= lo && 4 * l + 3 <= hi) mu1_bin<SPEC, 3>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
-  };
-  edge(l0);
-  for (int l = l0 + 1; l < l1; ++l) {                // interior lanes: 4 bins, no tests
-    mu1_bin<SPEC, 0>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
-    mu1_bin<SPEC, 1>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
-    mu1_bin<SPEC, 2>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
-    mu1_bin<SPEC, 3>(l, mu1, q_prev, ip, q1r, yr, m1r, ar);
+  for (int l = lo >> 2; l <= (hi >> 2); ++l) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * l + j;
+      if (i < lo || i > hi) continue;                // scalar: first and last lane only
+      const double a = mu1 * q_prev + readlane_f64(ip[j], l);
+      q_prev = readlane_f64(q1r[j], l);
+      const double y = readlane_f64(yr[j], l);
+      if (SPEC)
+        mu1 = fma(a, y, a * (fma(-q_prev, y, 1.0) * y));
+      else
+        mu1 = div_rn(a, q_prev, y);
+      if (lane == l) {
+        m1r[j] = mu1;
+        if (SPEC) ar[j] = a;
+      }
+    }
   }
-  if (l1 > l0) edge(l1);
 }
 
 __device__ double otsu_wave(const uint32_t* h, int64_t n) {
