@@ -21,7 +21,8 @@ duration is longer than the period at which they complete.
 ``--config c3``: the 36-view turntable scan (BASELINE configs[2]) as ONE job, views sharded
 across the ranks (strong scaling): every rank decodes its block, the clouds are gathered to rank
 0 through the C-ABI RCCL gatherv (``slg_gather_*``), the timed region includes it.
-``--config c4|c5``: the larger single-GPU geometries.  For N>1 on the default config each rank
+``--config c5job``: BASELINE configs[4], 8 objects x 72 views at 4K resident in HBM, one job per
+step (bench_c5job.py).  ``--config c4|c5``: the larger single-GPU geometries.  For N>1 on the default config each rank
 runs its own stream of views (weak scaling, no data-path collective); value = all ranks' points /
 max-over-ranks time.
 
@@ -62,30 +63,53 @@ CONFIGS = {
     "c5": dict(cam=(3840, 2160), proj=(1920, 1080), nsets=(11, 11), n_present=None, views=4, copies=2, batch=4,
                text="C5: 3840x2160 view, projector 1920x1080, 11 col + 11 row Gray bits + inverses + "
                     "white/black (46 frames)"),
+    "c5job": dict(cam=(3840, 2160), proj=(1920, 1080), nsets=(11, 11), n_present=None, views=576, copies=1, batch=4,
+                  text="C5 job: 8 objects x 72 views at 3840x2160, projector 1920x1080, 11 col + 11 row Gray bits "
+                       "+ inverses + white/black (46 frames), all views resident in HBM, one job per step, "
+                       "views sharded over the ranks"),
 }
+REF_CALIBRATION_OF = {"c5job": "c5"}     # workloads timed by tools/ref_vs_port.py under another name
 
 
 # ----------------------------------------------------------------------------- CPU baseline
 _CPU_JOB = None     # (views, calib, proj, nsets): inherited by the forked workers, never pickled
+MAX_CPU_WORKERS = 64        # host-memory bound of the pool (~1 GB per C2 worker, ~4 at 4K)
 
 
 def _cpu_worker(args):
-    """One host process: the oracle over views until `seconds` elapse -> (points, views, s)."""
+    """One host process: the reference's operation sequence (oracle/sl_refseq.py) over views
+    until `seconds` elapse -> (points, views, s)."""
     os.environ["OMP_NUM_THREADS"] = "1"
-    from oracle import sl_oracle as O
+    from oracle import sl_refseq as R
     seconds, first = args
     views, cal, proj, nsets = _CPU_JOB
     (PW, PH), (nc, nr) = proj, nsets
     done, pts, t0 = 0, 0, time.perf_counter()
     while True:
         v = views[(first + done) % len(views)]
-        col, row, mask = O.decode_processing(list(v.frames), n_cols=PW, n_rows=PH, n_sets_col=nc, n_sets_row=nr)
-        P, _ = O.reconstruct_processing(col, row, mask, v.texture, cal, row_mode=1)
+        col, row, mask, tex = R.gray_decode(list(v.frames), v.texture, n_cols=PW, n_rows=PH, n_sets_col=nc,
+                                            n_sets_row=nr)
+        P, _ = R.reconstruct(col, row, mask, tex, cal, row_mode=1)
         pts += len(P)
         done += 1
         if time.perf_counter() - t0 >= seconds:
             break
     return pts, done, time.perf_counter() - t0
+
+
+def ref_over_port(config: str):
+    """The committed calibration of the port against the reference itself for this workload
+    (tools/ref_vs_port.py -> profiles/r4_ref_vs_port.json, build container): reference time /
+    port time on the same views, or None."""
+    p = os.path.join(ROOT, "profiles", "r4_ref_vs_port.json")
+    try:
+        with open(p) as f:
+            c = json.load(f)["configs"].get(REF_CALIBRATION_OF.get(config, config))
+    except (OSError, ValueError, KeyError):
+        return None
+    return None if c is None else {"ref_over_port": c["ref_over_port"], "ref_over_oracle": c["ref_over_oracle"],
+                                   "median_s": c["median_s"], "views": c["views"],
+                                   "source": "profiles/r4_ref_vs_port.json (tools/ref_vs_port.py)"}
 
 
 def _cpu_model():
@@ -124,15 +148,21 @@ def _pool_rate(workers, seconds):
     return sum(r[0] for r in res), sum(r[1] for r in res), max(r[2] for r in res)
 
 
-def cpu_baseline(views, cal, seconds, wl):
-    """The oracle (NumPy restatement of the reference path, test infrastructure: in-memory
-    frames, prefix-XOR Gray decode, no imread) on this host: (i) one process, (ii) a process pool
-    with one stream of views per worker on every CPU the lease owns -- the affinity mask, capped
-    by the cgroup CPU quota when one is set (more processes than the quota only time-share it:
-    ``oversubscribed_2x`` measures that, with twice as many workers for half the time).  Runs
-    BEFORE the GPU is touched (fork-safe).  `value` is the pool figure, the stronger baseline."""
+def cpu_baseline(views, cal, seconds, wl, config: str):
+    """The reference CPU path on this host: ``oracle/sl_refseq.py``, the reference's own NumPy
+    operation sequence (``server/processing.py:49-234``: boolean-scatter bit planes, the
+    ``while np.any`` Gray loop, ``Nc[:, idx]`` gather, full-width temporaries; frames in memory,
+    no PNG decode; ``Nc`` Fortran-ordered as ``scipy.io.loadmat`` hands it over), timed (i) in one
+    process and (ii) on a process pool with one stream of views per worker on every CPU the lease
+    owns -- the affinity mask, capped by the cgroup CPU quota when one is set and by
+    ``MAX_CPU_WORKERS`` (more processes than the quota only time-share it: ``oversubscribed_2x``
+    measures that, with twice as many workers for half the time).  ``ref_over_port``: the
+    committed reference/port time ratio measured in the build container, where the reference
+    exists (tools/ref_vs_port.py).  Runs on rank 0 BEFORE the GPU is touched (fork-safe), at
+    every N.  ``value`` is the pool figure, the stronger baseline."""
     global _CPU_JOB
     import numpy as np
+    cal = dict(cal, Nc=np.asfortranarray(cal["Nc"]))
     _CPU_JOB = (views, cal, wl["proj"], wl["nsets"])
     nsets = wl["nsets"]
     one = _cpu_worker((seconds, 0))
@@ -141,10 +171,10 @@ def cpu_baseline(views, cal, seconds, wl):
     except AttributeError:
         avail = os.cpu_count() or 1
     quota = cpu_quota()
-    workers = max(1, min(avail, quota or avail))
+    workers = max(1, min(avail, quota or avail, MAX_CPU_WORKERS))
     pts, n_views, wall = _pool_rate(workers, seconds)
     over = None
-    if quota is not None and quota < avail:
+    if quota is not None and quota < avail and 2 * workers <= MAX_CPU_WORKERS:
         p2, v2, w2 = _pool_rate(min(avail, 2 * workers), seconds / 2)
         over = {"workers": min(avail, 2 * workers), "value": round(p2 / w2 / 1e6, 4), "views": v2,
                 "what": "2x the quota in worker processes, ~half the time: the quota, not the process "
@@ -153,12 +183,39 @@ def cpu_baseline(views, cal, seconds, wl):
     return {"value": round(pts / wall / 1e6, 4), "unit": "Mpoints/s", "cores": workers, "kind": "port",
             "sample": f"{n_views} {tag} views ({wl['cam'][0]}x{wl['cam'][1]}, {nsets[0]}+{nsets[1]} bits, Otsu, "
                       f"row_mode 1) on {workers} worker processes x ~{seconds:.0f} s, frames in memory",
-            "what": "oracle/sl_oracle.py: NumPy restatement of server/processing.py:28-234 (in-memory frames, "
-                    "prefix-XOR Gray decode, no imread), one view stream per process",
+            "what": "oracle/sl_refseq.py: the reference's NumPy operation sequence for server/processing.py:49-234 "
+                    "(in-memory frames, no PNG decode), one view stream per process",
+            "ref_calibration": ref_over_port(config),
             "single_process_value": round(one[0] / one[2] / 1e6, 4),
             "single_process_sample": f"{one[1]} views in {one[2]:.1f} s, 1 process",
             "host_cpus": os.cpu_count(), "cpus_available": avail, "cpu_quota": quota,
             "oversubscribed_2x": over, "cpu_model": _cpu_model(), "numpy": np.__version__}
+
+
+def rank0_cpu_baseline(args, rank: int, views, cal, wl):
+    """``cpu_baseline`` on rank 0 at every N (the other ranks wait at the rendezvous meanwhile),
+    None elsewhere or with ``--no-cpu-baseline``.  Must run before this process touches the GPU."""
+    if rank != 0 or args.no_cpu_baseline:
+        return None
+    t = time.perf_counter()
+    cpu = cpu_baseline(views, cal, args.cpu_seconds, wl, args.config)
+    log(f"[rank 0] cpu baseline {cpu['value']} Mpts/s on {cpu['cores']} processes "
+        f"({cpu['single_process_value']} on 1) in {time.perf_counter() - t:.1f}s")
+    return cpu
+
+
+def cpu_baseline_only(args, rank: int, world: int, cpu) -> None:
+    """``--cpu-baseline-only``: the JSON line with the CPU baseline and no GPU part (any host;
+    the ranks still rendezvous over gloo so a spawned run behaves as the GPU one does)."""
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpoints/s", "n_gpus": world,
+                          "config": {"workload": CONFIGS[args.config]["text"]}, "cpu_baseline": cpu}),
+              file=getattr(args, "result_out", None) or RESULT_OUT, flush=True)
 
 
 def load_traffic_per_view():
@@ -261,6 +318,9 @@ def main():
     ap.add_argument("--copies", type=int, default=None, help="device copies of each view in the pool")
     ap.add_argument("--batch", type=int, default=None, help="views per fused launch (<= 16)")
     ap.add_argument("--xyz", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--objects", type=int, default=8, help="c5job: objects in the job")
+    ap.add_argument("--views-per-object", type=int, default=72, help="c5job: turntable views per object")
+    ap.add_argument("--distinct", type=int, default=1, help="c5job: rendered captures per object")
     ap.add_argument("--pipeline", choices=["serial", "overlap", "fused", "fused2"], default="fused2",
                     help="serial: stats + fused launch per batch on one stream; overlap: the next "
                          "batch's stats on a side stream during this batch's fused launch; fused: "
@@ -272,6 +332,8 @@ def main():
                     help="HIP events per fused launch, or one pair around the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-only", action="store_true",
+                    help="print the JSON line with the CPU baseline alone (no GPU is touched)")
     ap.add_argument("--no-verify", action="store_true")
     args = ap.parse_args()
     mode = launch_mode(args.gpus, os.environ)
@@ -287,10 +349,13 @@ def main():
     for k in ("views", "copies", "batch"):
         if getattr(args, k) is None:
             setattr(args, k, wl[k])
+    args.result_out = RESULT_OUT         # (bench_c3 imports this file as module "bench")
     if args.config == "c3":
-        args.result_out = RESULT_OUT
         import bench_c3
         return bench_c3.main(args, wl)
+    if args.config == "c5job":
+        import bench_c5job
+        return bench_c5job.main(args, wl)
 
     import numpy as np
     import torch
@@ -309,12 +374,9 @@ def main():
     views = [synth.render_view(rig, view_deg=(rank * args.views + i) * 360.0 / (world * args.views),
                                seed=1000 * rank + i, n_present=wl["n_present"]) for i in range(args.views)]
     log(f"[rank {rank}] rendered {len(views)} views in {time.perf_counter() - t:.1f}s")
-    cpu = None
-    if world == 1 and rank == 0 and not args.no_cpu_baseline:   # before the GPU is touched
-        t = time.perf_counter()
-        cpu = cpu_baseline(views, cal, args.cpu_seconds, wl)
-        log(f"[rank 0] cpu baseline {cpu['value']} Mpts/s on {cpu['cores']} processes "
-            f"({cpu['single_process_value']} on 1) in {time.perf_counter() - t:.1f}s")
+    cpu = rank0_cpu_baseline(args, rank, views, cal, wl)          # before the GPU is touched
+    if args.cpu_baseline_only:
+        return cpu_baseline_only(args, rank, world, cpu)
 
     # Rehearsal knobs for the multi-rank path on a one-GPU box (never set by the driver):
     # SLG_BENCH_DEVICE pins every rank to one device, SLG_BENCH_BACKEND=gloo replaces RCCL.

@@ -100,12 +100,39 @@ def gather_clouds(xyz: torch.Tensor, bgr: torch.Tensor, dst: int = 0):
     return out
 
 
+BAD_SLOT = -1       # width slot of a rank whose gather arguments are invalid
+
+
+def local_gather_row(clouds, n_per_rank: int, xyz_dtype=None) -> list[int]:
+    """This rank's row of the count table: ``n_per_rank`` view counts (-1 = padding slot), then
+    the XYZ element width (0 = no views).  Invalid arguments (more views than ``n_per_rank``,
+    mixed XYZ widths, a dtype other than ``xyz_dtype``) put ``BAD_SLOT`` in the width slot
+    instead of raising here: the counts all-gather is a collective, so a rank that raised before
+    it would leave its peers blocked in it.  :func:`gather_plan` raises on every rank."""
+    row = [-1] * (n_per_rank + 1)
+    widths = {x.element_size() for x, _ in clouds}
+    if (len(clouds) > n_per_rank or len(widths) > 1
+            or (xyz_dtype is not None and any(x.dtype != xyz_dtype for x, _ in clouds))):
+        row[n_per_rank] = BAD_SLOT
+        return row
+    for k, (x, _) in enumerate(clouds):
+        row[k] = int(x.shape[0])
+    row[n_per_rank] = widths.pop() if widths else 0
+    return row
+
+
 def gather_plan(table, n_per_rank: int, xyz_dtype=None):
     """The root's view of a gather from the all-gathered count table (host logic of
     :meth:`RcclCloudGather.gather`, testable without RCCL).  ``table[r]`` is rank r's
     ``n_per_rank`` view counts (-1 = padding slot) followed by its XYZ element width in bytes (0
-    when it holds no views).  Returns ``(xyz dtype, counts)`` with ``counts[r]`` the real views'
-    point counts of rank r; raises ``ValueError`` when ranks disagree on the width."""
+    when it holds no views, ``BAD_SLOT`` when the rank's own arguments are invalid).  Returns
+    ``(xyz dtype, counts)`` with ``counts[r]`` the real views' point counts of rank r; raises
+    ``ValueError`` -- on every rank alike, since every rank holds the same table -- when a rank
+    flagged its arguments or ranks disagree on the width."""
+    bad = [r for r, row in enumerate(table) if int(row[n_per_rank]) == BAD_SLOT]
+    if bad:
+        raise ValueError(f"rank(s) {bad} passed more views than n_per_rank or clouds of mixed "
+                         f"XYZ dtypes (or not of xyz_dtype)")
     seen = {int(row[n_per_rank]) for row in table} - {0}
     if xyz_dtype is not None:
         seen.add(torch.empty(0, dtype=xyz_dtype).element_size())
@@ -159,21 +186,15 @@ class RcclCloudGather:
         The XYZ dtype is agreed across ranks, not guessed from a possibly empty list: every rank
         sends its element width with its counts (0 when it holds no views), ``xyz_dtype``
         (optional) fixes it, and ranks holding clouds of different widths raise ``ValueError``
-        on every rank before any byte moves."""
+        on every rank before any byte moves.  So do invalid arguments on any one rank (more
+        views than ``n_per_rank``, mixed widths): they travel as a flag in the count table, and
+        every rank raises after the counts all-gather instead of one rank raising before it."""
         N, ct = self.N, self.ct
-        if len(clouds) > n_per_rank:
-            raise ValueError("more views than n_per_rank")
-        widths = {x.element_size() for x, _ in clouds}
-        if len(widths) > 1 or (xyz_dtype is not None and clouds and clouds[0][0].dtype != xyz_dtype):
-            raise ValueError("this rank's clouds mix XYZ dtypes (or differ from xyz_dtype)")
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         sp = ct.c_void_p(s.cuda_stream)
         slots = n_per_rank + 1                    # per rank: view counts (-1 = padding), XYZ width
         with torch.cuda.stream(s):
-            cnt = torch.full((slots,), -1, dtype=torch.int64, device=self.device)
-            for k, (x, _) in enumerate(clouds):
-                cnt[k] = x.shape[0]
-            cnt[n_per_rank] = clouds[0][0].element_size() if clouds else 0
+            cnt = torch.tensor(local_gather_row(clouds, n_per_rank, xyz_dtype), dtype=torch.int64).to(self.device)
             allc = torch.empty(self.world * slots, dtype=torch.int64, device=self.device)
             N.check(N.lib().slg_gather_counts(self.comm, ct.c_void_p(cnt.data_ptr()), slots,
                                               ct.c_void_p(allc.data_ptr()), sp))

@@ -155,7 +155,12 @@ class DeviceCalib:
         self.ray_mode = N.RAYS_PINHOLE
         self.table_is_pinhole = None
         if Nc.ndim == 2 and Nc.shape[1] == self.height * self.width:
-            rays = torch.from_numpy(np.ascontiguousarray(Nc, dtype=np.float64)).to(device)
+            if Nc.dtype == np.float64 and not Nc.flags.c_contiguous and Nc.flags.f_contiguous:
+                # loadmat's Fortran-ordered table: upload its C-contiguous transpose as it lies
+                # in host memory and transpose on the device (no host copy of up to 576 MB)
+                rays = torch.from_numpy(Nc.T).to(device).t().contiguous()
+            else:
+                rays = torch.from_numpy(np.ascontiguousarray(Nc, dtype=np.float64)).to(device)
             mism = torch.zeros(1, dtype=torch.int64, device=device)
             N.check(N.lib().slg_rays_match_pinhole(_vp(rays), self.height, self.width, self.fx,
                                                    self.fy, self.cx, self.cy, _vp(mism), _stream()))
@@ -351,6 +356,12 @@ class PreparedBatch:
         return (self.n + MAX_VIEWS_PER_LAUNCH - 1) // MAX_VIEWS_PER_LAUNCH
 
 
+def same_decode(a: PreparedBatch, b: PreparedBatch) -> bool:
+    """Whether two prepared batches decode with identical parameters (``DecodeParams`` bytes):
+    a fused launch that carries or finishes another batch applies its own parameters to it."""
+    return bytes(a.dp) == bytes(b.dp)
+
+
 class BatchReconstructor:
     """Many views of one geometry per call (``process_multi_ply(mode='batch')``,
     server/processing.py:314-334): per group of up to 16 views one batched stats launch and ONE
@@ -427,6 +438,8 @@ class BatchReconstructor:
         slot) into the slot's per-tile partials (``slg_decode_triangulate_batch_next``)."""
         if nxt.slot != pb.slot or nxt.n > pb.n:
             raise ValueError("the carried batch must use this batch's slot and have no more views")
+        if not same_decode(nxt, pb):
+            raise ValueError("the carried batch must share this batch's decode parameters")
         N.check(N.lib().slg_decode_triangulate_batch_next(
             pb.caps, pb.n, ctypes.byref(pb.dp), ctypes.byref(pb.calib), ctypes.byref(pb.tp), self._ws(pb.slot),
             self.ws_stride, pb.clouds, nxt.caps, nxt.n, self._events_arg(pb, events), _stream(stream)))
@@ -441,6 +454,11 @@ class BatchReconstructor:
             raise ValueError("the carried batch must use this batch's slot and have no more views")
         if fin is not None and (fin.slot == pb.slot or fin.n > MAX_VIEWS_PER_LAUNCH):
             raise ValueError("the finished batch must use another slot and have <= 16 views")
+        # the launch turns fin's partials into thresholds and counts nxt's histograms with pb's
+        # decode parameters; the C side cannot tell them apart, so they must be the same
+        for other, what in ((nxt, "carried"), (fin, "finished")):
+            if other is not None and not same_decode(other, pb):
+                raise ValueError(f"the {what} batch must share this batch's decode parameters")
         N.check(N.lib().slg_decode_triangulate_batch_carry(
             pb.caps, pb.n, ctypes.byref(pb.dp), ctypes.byref(pb.calib), ctypes.byref(pb.tp), self._ws(pb.slot),
             self.ws_stride, pb.clouds, nxt.caps if nxt is not None else None, nxt.n if nxt is not None else 0,
@@ -472,8 +490,9 @@ class BatchReconstructor:
             raise ValueError("fused2 needs Otsu thresholds")
         streams = (s0, s1)
 
-        def carried(j):          # batch j's histograms ride on launch j-4
-            return (j >= 4 and batches[j].n <= batches[j - 4].n and batches[j].n <= MAX_VIEWS_PER_LAUNCH)
+        def carried(j):          # batch j's histograms ride on launch j-4, launch j-2 finishes them
+            return (j >= 4 and batches[j].n <= batches[j - 4].n and batches[j].n <= MAX_VIEWS_PER_LAUNCH
+                    and same_decode(batches[j], batches[j - 4]) and same_decode(batches[j], batches[j - 2]))
 
         if start == 0:
             for k in range(min(4, n)):
@@ -488,9 +507,11 @@ class BatchReconstructor:
 
     @staticmethod
     def _carried(batches, j) -> bool:
-        """Whether batch j's histograms ride on batch j-2's fused launch (same slot, no more views)."""
+        """Whether batch j's histograms ride on batch j-2's fused launch (same slot, no more views)
+        and batch j-1's launch finishes them (all three decode with the same parameters)."""
         return (j >= 2 and batches[j].slot == batches[j - 2].slot and batches[j].n <= batches[j - 2].n
-                and batches[j].n <= MAX_VIEWS_PER_LAUNCH)
+                and batches[j].n <= MAX_VIEWS_PER_LAUNCH
+                and same_decode(batches[j], batches[j - 2]) and same_decode(batches[j], batches[j - 1]))
 
     def run_pipelined(self, batches, main_stream, stats_stream=None, events=None, mode="fused",
                       start=0, stop=None):

@@ -189,11 +189,18 @@ class FormattedCloud:
     body: torch.Tensor              # pinned uint8, the first `length` bytes are the body
     length: int
     pool: PinnedPool
+    released: bool = False
 
     def write(self, filename) -> None:
         try:
             PLY.write_body(filename, self.n_points, self.body[: self.length].numpy())
         finally:
+            self.release()
+
+    def release(self) -> None:
+        """Return the pinned body to the pool (once; later calls do nothing)."""
+        if not self.released:
+            self.released = True
             self.pool.put(self.body)
 
 
@@ -377,5 +384,8 @@ class BatchPipeline:
                     continue
                 except Exception as e:  # noqa: BLE001
                     err = e
+                finally:                # a write stage that never called r.write() (or failed
+                    if isinstance(r, FormattedCloud):   # before it) still returns the buffer
+                        r.release()
             log(f"  ❌ Error in {name}: {err}\n")
         return ok

@@ -43,13 +43,27 @@ def _hasher():
 _NC_SAMPLE = 1 << 16                        # Nc elements hashed by the cheap fingerprint
 
 
+def _logical_sample(a: np.ndarray, idx: np.ndarray) -> np.ndarray:
+    """``a.reshape(-1)[idx]`` (C order) without copying ``a``: a flat view when ``a`` is
+    C-contiguous, its transpose's flat view when it is a Fortran-ordered 2-D table."""
+    if a.flags.c_contiguous:
+        return a.reshape(-1)[idx]
+    if a.ndim == 2 and a.flags.f_contiguous:
+        r, c = np.divmod(idx, a.shape[1])
+        return a.T.reshape(-1)[c * a.shape[0] + r]
+    return a[np.unravel_index(idx, a.shape)]
+
+
 def calib_fingerprint(calib, full: bool = False) -> str:
     """Digest of the calibration arrays the path reads (xxh3 over shapes, dtypes and bytes).
 
     ``cam_K``, ``Oc`` and the plane tables (<= 131 KB) are always hashed whole.  ``Nc`` (3 x H*W
     float64: 50 MB at 1080p, 576 MB at 24 MP) is hashed whole only with ``full=True``; the cheap
     form hashes its shape, dtype and a strided sample of 65536 elements (first and last
-    included), which costs well under a millisecond at any size."""
+    included, taken by logical index so a Fortran-ordered table -- what ``scipy.io.loadmat``
+    returns -- is neither copied nor hashed differently from its C-ordered twin), which costs
+    well under a millisecond at any size.  The full form hashes a Fortran-ordered table through
+    its C-contiguous transpose (no copy either) and tags the order in the digest."""
     h = _hasher()
     for k in ("cam_K", "Oc", "wPlaneCol", "wPlaneRow", "Nc"):
         a = calib.get(k) if hasattr(calib, "get") else None
@@ -58,9 +72,12 @@ def calib_fingerprint(calib, full: bool = False) -> str:
             continue
         a = np.asarray(a)
         h.update(f"{k}:{a.shape}:{a.dtype.str};".encode())
-        if k == "Nc" and not full and a.size > _NC_SAMPLE:
-            flat = a.reshape(-1)            # a view for the contiguous table loadmat returns
-            a = flat[np.linspace(0, flat.size - 1, _NC_SAMPLE).astype(np.int64)]
+        if k == "Nc" and a.size > _NC_SAMPLE:
+            if not full:
+                a = _logical_sample(a, np.linspace(0, a.size - 1, _NC_SAMPLE).astype(np.int64))
+            elif a.ndim == 2 and not a.flags.c_contiguous and a.flags.f_contiguous:
+                h.update(b"F;")
+                a = a.T                                # C-contiguous view of the same bytes
         h.update(memoryview(np.ascontiguousarray(a)).cast("B"))
     return h.hexdigest()
 

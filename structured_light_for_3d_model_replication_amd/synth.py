@@ -226,6 +226,33 @@ def render_view(rig: Rig, view_deg: float = 0.0, seed: int = 0, n_present: int |
                 lit=lit.reshape(H, W))
 
 
+_RIG = None         # the rig of render_many's forked workers (inherited, never pickled)
+
+
+def _render_spec(spec):
+    deg, seed, n_present = spec
+    return render_view(_RIG, view_deg=deg, seed=seed, n_present=n_present)
+
+
+def render_many(rig: Rig, specs, workers: int = 1) -> list:
+    """``render_view`` for each ``(view_deg, seed, n_present)`` spec, on ``workers`` forked
+    processes (host only: call it before the process touches a GPU)."""
+    global _RIG
+    specs = list(specs)
+    if workers <= 1 or len(specs) <= 1:
+        return [render_view(rig, view_deg=d, seed=s, n_present=n) for d, s, n in specs]
+    import multiprocessing as mp
+    _RIG = rig
+    with mp.get_context("fork").Pool(min(workers, len(specs))) as pool:
+        return pool.map(_render_spec, specs, chunksize=1)
+
+
+def job_view_angle(obj: int, view: int, n_views: int) -> float:
+    """Turntable angle of view ``view`` of object ``obj`` in a scan-farm job (objects start at
+    staggered angles so no two objects' captures coincide)."""
+    return 360.0 * view / n_views + 45.0 * obj
+
+
 def write_capture(view: View, folder: str, ext: str = "png") -> list[str]:
     """Write the frames in the reference's capture layout ``01.png, 02.png, ...``
     (``server/sl_system.py:444-459``) as 8-bit grayscale files; returns the file list.

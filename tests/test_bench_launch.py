@@ -53,6 +53,23 @@ def test_spawn_ranks_env_and_stdout(tmp_path):
     assert '"rank": 1' in r.stderr
 
 
+@pytest.mark.parametrize("config", ["c2", "c3"])
+def test_spawned_two_rank_line_carries_cpu_baseline(config):
+    """``bench.py --gpus 2`` (self-spawned ranks, the driver's N>1 lines): rank 0 times the
+    reference CPU path before touching the GPU, so the N>1 line carries ``cpu_baseline`` too
+    (``--cpu-baseline-only`` stops there; no GPU is needed)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", config,
+                        "--views", "1" if config == "c2" else "2", "--cpu-seconds", "0.2", "--cpu-baseline-only"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 2
+    cpu = lines[0]["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["kind"] == "port" and cpu["cores"] >= 1
+    assert "sl_refseq" in cpu["what"]
+
+
 def test_spawn_ranks_propagates_failure(tmp_path):
     script = tmp_path / "fail.py"
     script.write_text("import os, sys\nsys.exit(3 if os.environ['RANK'] == '1' else 0)\n")

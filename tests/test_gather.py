@@ -72,6 +72,63 @@ def test_gather_plan_agrees_dtype_and_drops_padding():
         D.gather_plan([[5, 4], [-1, 0]], 1, torch.float64)
 
 
+def test_local_gather_row_flags_bad_arguments():
+    """Invalid arguments on one rank become a flag in its count row (no local raise before the
+    collective); the plan then raises on every rank alike."""
+    from structured_light_for_3d_model_replication_amd import distributed as D
+    f32 = (torch.zeros((3, 3), dtype=torch.float32), torch.zeros((3, 3), dtype=torch.uint8))
+    f64 = (torch.zeros((2, 3), dtype=torch.float64), torch.zeros((2, 3), dtype=torch.uint8))
+    assert D.local_gather_row([f32, f32], 3) == [3, 3, -1, 4]
+    assert D.local_gather_row([], 2) == [-1, -1, 0]
+    for clouds, dt in (([f32, f32, f32], None),     # more views than n_per_rank
+                       ([f32, f64], None),          # mixed widths
+                       ([f32], torch.float64)):     # not of the agreed dtype
+        row = D.local_gather_row(clouds, 2, dt)
+        assert row[2] == D.BAD_SLOT
+        table = [row, D.local_gather_row([f64], 2)]
+        with pytest.raises(ValueError, match="rank"):
+            D.gather_plan(table, 2)
+
+
+def _gloo_bad_rank_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from structured_light_for_3d_model_replication_amd import distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        x = (torch.zeros((4, 3), dtype=torch.float32), torch.zeros((4, 3), dtype=torch.uint8))
+        clouds = [x, x, x] if rank == 1 else [x]          # rank 1 passes too many views
+        row = torch.tensor(D.local_gather_row(clouds, 2), dtype=torch.int64)
+        rows = [torch.empty_like(row) for _ in range(world)]
+        dist.all_gather(rows, row)                         # every rank reaches the collective
+        try:
+            D.gather_plan([r.tolist() for r in rows], 2)
+            q.put((rank, "no error"))
+        except ValueError as e:
+            q.put((rank, "ValueError" if "[1]" in str(e) else str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_bad_rank_raises_on_every_rank_gloo():
+    """World size 2 over gloo: rank 1's invalid arguments make BOTH ranks raise after the counts
+    all-gather -- none is left waiting in the collective."""
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_bad_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert sorted(q.get(timeout=5) for _ in range(2)) == [(0, "ValueError"), (1, "ValueError")]
+
+
 # ------------------------------------------------------------------------------------- GPU
 def _rank_clouds(rank, case, f64):
     """Deterministic ragged clouds per (rank, case): list of (xyz, bgr) numpy arrays."""

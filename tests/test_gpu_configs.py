@@ -205,3 +205,48 @@ def test_c5_full_size(mods):
         P, C = o.result()
         assert len(P) == len(Pw) and np.array_equal(C.cpu().numpy(), Cw)
         _xyz32_close(P.cpu().numpy(), Pw)
+
+
+def test_c5_resident_job(mods):
+    """BASELINE configs[4] reduced to 2 objects x 4 views (bench.py --config c5job's code path,
+    jobs.ResidentJob): 3840x2160 views, each an HBM copy of one of 2 captures per object, one
+    fused launch per view on the two-stream carried pipeline (4 primed + 4 carried groups), the
+    clouds packed in one arena by capacity hints.  Every view's count and colours equal the
+    oracle's, XYZ within the north-star tolerance; a view given too small a hint is reported as
+    overflowed (its stores stay inside the arena)."""
+    E, N = mods
+    import torch
+    from structured_light_for_3d_model_replication_amd import jobs as J, synth
+    H, W = 2160, 3840
+    rig = synth.default_rig(W, H, 1920, 1080)
+    cal = rig.tables()
+    keys = [(o, k) for o in range(2) for k in range(2)]
+    with ThreadPoolExecutor(4) as ex:
+        caps = list(ex.map(lambda ok: synth.render_view(rig, synth.job_view_angle(ok[0], 2 * ok[1], 4),
+                                                        seed=1000 * ok[0] + ok[1]), keys))
+    want = _oracle_all(cal, caps, (11, 11))
+    cfg = E.DecodeConfig(1920, 1080, 11, 11, "otsu")
+    dcal = E.DeviceCalib(cal, H, W)
+    sources = [E.DeviceFrames(list(v.frames), v.texture) for v in caps]
+    plan = [2 * o + a * 2 // 4 for o in range(2) for a in range(4)]       # source of job view j
+    views = J.stage_copies(sources, plan)
+    del sources
+    hints = [len(want[p][0]) for p in plan]
+    job = J.ResidentJob(views, cfg, dcal, batch=1, capacity_hints=hints)
+    s0, s1 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(2):                                  # a job re-run rewrites the same clouds
+        job.run(s0, s1)
+    torch.cuda.synchronize()
+    counts = job.host_counts()
+    assert counts == hints and job.overflowed(counts) == []
+    assert len(job.batches) == 8 and job.xyz.shape[0] == sum(hints) + H * W
+    for j, p in enumerate(plan):
+        x, b = job.cloud(j, counts)
+        assert np.array_equal(b.cpu().numpy(), want[p][1]), j
+        _xyz32_close(x.cpu().numpy(), want[p][0])
+    small = list(hints)
+    small[2] -= 1000                                    # view 2 cannot fit: flagged, not faulted
+    job2 = J.ResidentJob(views[:4], cfg, dcal, batch=2, capacity_hints=small[:4])
+    job2.run(s0, s1)
+    torch.cuda.synchronize()
+    assert job2.overflowed() == [2]

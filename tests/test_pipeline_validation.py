@@ -1,0 +1,113 @@
+"""Host-side invariants of the carried-histogram pipelines (engine.BatchReconstructor.run_pipelined,
+modes "fused" / "fused2"): which batch's histograms ride on which launch, which launch finishes
+them, and that a batch decoding with other parameters is never carried or finished by a launch
+that would apply the wrong ones (the C side cannot tell).  CPU only: the native calls are replaced
+by recorders, so these run without a GPU.  The reference's batch loop is serial
+(server/processing.py:319-330); the pipeline is this build's scheduling of it."""
+import pytest
+
+from structured_light_for_3d_model_replication_amd import _native as N
+from structured_light_for_3d_model_replication_amd import engine as E
+
+
+def _batch(slot, n=4, mode=N.THRESH_OTSU, n_sets_col=11):
+    dp = N.DecodeParams(proj_cols=1920, proj_rows=1080, n_sets_col=n_sets_col, n_sets_row=10,
+                        variant=N.VARIANT_PROCESSING, thresh_mode=mode, shadow_val=40.0, contrast_val=10.0)
+    return E.PreparedBatch(caps=None, n=n, dp=dp, calib=None, tp=None, clouds=None, slot=slot, outs=[])
+
+
+class _Rec(E.BatchReconstructor):
+    """A BatchReconstructor whose launches are recorded instead of issued."""
+
+    def __init__(self):                       # no device, no workspace
+        self.calls = []
+
+    def stats(self, pb, stream=None):
+        self.calls.append(("stats", pb, stream))
+
+    def main_carry(self, pb, nxt, fin, events=None, stream=None):
+        self.calls.append(("carry", pb, nxt, fin, stream))
+
+
+def _carry_calls(rec):
+    return [c for c in rec.calls if c[0] == "carry"]
+
+
+def test_fused2_carries_k_plus_4_and_finishes_k_plus_2():
+    rec = _Rec()
+    bs = [_batch(k % 4) for k in range(10)]
+    rec.run_pipelined(bs, "s0", "s1", mode="fused2")
+    stats = [c[1] for c in rec.calls if c[0] == "stats"]
+    assert stats == bs[:4]                                # only the first four get a stats pass
+    for k, (_, pb, nxt, fin, s) in enumerate(_carry_calls(rec)):
+        assert pb is bs[k] and s == ("s0", "s1")[k % 2]
+        assert nxt is (bs[k + 4] if k + 4 < 10 else None)
+        assert fin is (bs[k + 2] if 4 <= k + 2 < 10 else None)
+
+
+def test_fused2_never_carries_a_batch_with_other_decode_parameters():
+    rec = _Rec()
+    bs = [_batch(k % 4) for k in range(10)]
+    bs[6] = _batch(2, n_sets_col=10)                      # batch 6 decodes with other bit counts
+    rec.run_pipelined(bs, "s0", "s1", mode="fused2")
+    carry = _carry_calls(rec)
+    assert carry[2][2] is None and carry[4][3] is None    # neither carried by 2 nor finished by 4
+    assert ("stats", bs[6], "s0") in rec.calls            # ... it gets a regular pass instead
+    # and batch 6 does not carry / finish batches with the common parameters either
+    assert carry[6][2] is None                            # batch 10 would not exist; 8's fin:
+    assert carry[6][3] is bs[8] or carry[6][3] is None
+    assert all(same for same in (E.same_decode(c[1], c[2]) for c in carry if c[2] is not None))
+    assert all(same for same in (E.same_decode(c[1], c[3]) for c in carry if c[3] is not None))
+
+
+def test_fused_one_stream_rejects_mixed_parameters_the_same_way():
+    rec = _Rec()
+    bs = [_batch(k % 2) for k in range(6)]
+    bs[3] = _batch(1, mode=N.THRESH_MANUAL)
+    bs[3].dp.thresh_mode = N.THRESH_OTSU                  # same mode, other thresholds below
+    bs[3].dp.shadow_val = 41.0
+    rec.run_pipelined(bs, "s", mode="fused")
+    carry = _carry_calls(rec)
+    assert carry[1][2] is None and carry[2][3] is None
+    assert ("stats", bs[3], "s") in rec.calls
+
+
+def test_fused2_slot_rules():
+    rec = _Rec()
+    with pytest.raises(ValueError, match="four different slots"):
+        rec.run_pipelined([_batch(k % 3) for k in range(6)], "s0", "s1", mode="fused2")
+    with pytest.raises(ValueError, match="second stream"):
+        rec.run_pipelined([_batch(k % 4) for k in range(6)], "s0", None, mode="fused2")
+    with pytest.raises(ValueError, match="Otsu"):
+        rec.run_pipelined([_batch(k % 4, mode=N.THRESH_MANUAL) for k in range(6)], "s0", "s1", mode="fused2")
+
+
+def test_main_carry_rejects_other_parameters_before_any_launch():
+    eng = E.BatchReconstructor.__new__(E.BatchReconstructor)
+    pb, other = _batch(0), _batch(1, n_sets_col=9)
+    with pytest.raises(ValueError, match="finished batch must share"):
+        eng.main_carry(pb, None, other)
+    with pytest.raises(ValueError, match="carried batch must share"):
+        eng.main_carry(pb, _batch(0, n_sets_col=9), None)
+    with pytest.raises(ValueError, match="carried batch must share"):
+        eng.main_next(pb, _batch(0, n_sets_col=9))
+
+
+def test_packed_clouds_keep_the_capacity_contract():
+    """jobs.packed_clouds: view j's region starts at sum(hints[:j]); the arena ends with H*W
+    points of slack, so every view has >= H*W points to the arena's end (slg_cloud.capacity's
+    contract) and no store can leave the allocation, whatever the counts."""
+    import torch
+    from structured_light_for_3d_model_replication_amd import jobs as J
+    n_px = 1000
+    hints = [700, 0, 1000, 5]
+    clouds, offs, xyz, bgr, counts = J.packed_clouds(n_px, hints, device="cpu")
+    assert offs == [0, 700, 700, 1700, 1705] and xyz.shape == (1705 + n_px, 3) and bgr.shape == xyz.shape
+    for j, c in enumerate(clouds):
+        assert c.capacity == xyz.shape[0] - offs[j] >= n_px
+        assert c.xyz.data_ptr() == xyz[offs[j]:].data_ptr() and c.bgr.data_ptr() == bgr[offs[j]:].data_ptr()
+        assert c.count.data_ptr() == counts[j:].data_ptr() and c.xyz.dtype == torch.float32
+    _, _, x64, _, _ = J.packed_clouds(n_px, hints, xyz_f64=True, device="cpu")
+    assert x64.dtype == torch.float64
+    with pytest.raises(ValueError):
+        J.packed_clouds(n_px, [3, -1], device="cpu")

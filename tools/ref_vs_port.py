@@ -1,0 +1,124 @@
+#!/usr/bin/env python
+"""Calibrate the CPU-baseline port against the reference itself (build container only).
+
+Times, on the same rendered views with frames in memory (no PNG decode on either side):
+* ``ref``    -- the reference's ``ProcessingLogic._gray_decode`` + ``_reconstruct_point_cloud``
+  (``/root/reference/server/processing.py:28-234``), imported through
+  ``tests/golden/refharness.py`` (cv2 stubs: ``imread`` hands out a copy of the in-memory frame,
+  ``threshold`` runs the oracle's restatement of OpenCV's Otsu);
+* ``port``   -- ``oracle/sl_refseq.py``, the reference's operation sequence restated: what
+  ``bench.py``'s ``cpu_baseline`` times on the GPU box, where the reference does not exist;
+* ``oracle`` -- ``oracle/sl_oracle.py`` (the checker), for comparison.
+
+Median of ``--reps`` per leg, legs interleaved per repetition, one process, 1 BLAS thread.  The
+calibration is ``calibrate_final``-shaped with ``Nc`` Fortran-ordered, as ``scipy.io.loadmat``
+returns it to the reference (``server/processing.py:279-284``).  Every leg's output is checked
+equal to the reference's.  Writes a JSON summary (``--out``, default
+``profiles/r4_ref_vs_port.json``; configs already in it and not re-timed are kept).  Run it on an
+otherwise idle host.  ``/root/reference`` must exist: never run on the GPU box.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import statistics
+import sys
+import time
+
+os.environ.setdefault("OMP_NUM_THREADS", "1")
+os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+
+import numpy as np  # noqa: E402
+
+WORKLOADS = {
+    "c2": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 10), n_present=44),
+    "c3": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 11), n_present=None),
+    "c4": dict(cam=(6000, 4000), proj=(3840, 2160), nsets=(12, 12), n_present=None),
+    "c5": dict(cam=(3840, 2160), proj=(1920, 1080), nsets=(11, 11), n_present=None),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c2,c4,c5")
+    ap.add_argument("--views", type=int, default=2, help="rendered views per config (timed in turn)")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r4_ref_vs_port.json"))
+    args = ap.parse_args()
+
+    import refharness
+    from oracle import sl_oracle as O
+    from oracle import sl_refseq as R
+    from structured_light_for_3d_model_replication_amd import synth
+    PL = refharness.load()[0]
+
+    result = {"what": __doc__.strip().splitlines()[0], "host": platform.node(), "cpu": platform.processor(),
+              "numpy": np.__version__, "reps": args.reps, "configs": {}}
+    if os.path.exists(args.out):                      # configs timed by an earlier run are kept
+        with open(args.out) as f:
+            result["configs"] = json.load(f).get("configs", {})
+    for name in args.configs.split(","):
+        wl = WORKLOADS[name]
+        (W, H), (PW, PH), (nc, nr) = wl["cam"], wl["proj"], wl["nsets"]
+        rig = synth.default_rig(W, H, PW, PH)
+        cal = rig.tables()
+        cal["Nc"] = np.asfortranarray(cal["Nc"])
+        times = {"ref": [], "port": [], "oracle": []}
+        points = []
+        for v in range(args.views):
+            t = time.perf_counter()
+            view = synth.render_view(rig, view_deg=40.0 * v, seed=v, n_present=wl["n_present"])
+            print(f"[{name}] view {v} rendered in {time.perf_counter() - t:.1f}s", file=sys.stderr, flush=True)
+            frames = list(view.frames)
+            paths = refharness.register_frames(f"/mem/{name}/{v}", frames, view.texture)
+
+            def ref():
+                c, r, m, tex = PL._gray_decode(paths, n_cols=PW, n_rows=PH, n_sets_col=nc, n_sets_row=nr)
+                return PL._reconstruct_point_cloud(c, r, m, tex, cal, row_mode=1, epipolar_tol=2.0)
+
+            def port():
+                c, r, m, tex = R.gray_decode(frames, view.texture, n_cols=PW, n_rows=PH, n_sets_col=nc,
+                                             n_sets_row=nr)
+                return R.reconstruct(c, r, m, tex, cal, row_mode=1, epipolar_tol=2.0)
+
+            def oracle():
+                c, r, m = O.decode_processing(frames, n_cols=PW, n_rows=PH, n_sets_col=nc, n_sets_row=nr)
+                return O.reconstruct_processing(c, r, m, view.texture, cal, row_mode=1)
+
+            want = None
+            for rep in range(args.reps):
+                for leg, fn in (("ref", ref), ("port", port), ("oracle", oracle)):
+                    t = time.perf_counter()
+                    P, C = fn()
+                    times[leg].append(time.perf_counter() - t)
+                    if want is None:
+                        want = (P, C)
+                    elif rep == 0:
+                        assert np.array_equal(P, want[0]) and np.array_equal(C, want[1]), f"{name}: {leg} differs"
+            points.append(len(want[0]))
+            refharness._FRAMES.clear()
+            refharness._TEXTURES.clear()
+        med = {k: statistics.median(v) for k, v in times.items()}
+        pts = float(np.mean(points))
+        result["configs"][name] = {
+            "camera": f"{W}x{H}", "projector": f"{PW}x{PH}", "bits": f"{nc}+{nr}", "row_mode": 1,
+            "views": args.views, "points_per_view": int(pts),
+            "median_s": {k: round(v, 4) for k, v in med.items()},
+            "mpts_per_s": {k: round(pts / v / 1e6, 3) for k, v in med.items()},
+            "ref_over_port": round(med["ref"] / med["port"], 4),
+            "ref_over_oracle": round(med["ref"] / med["oracle"], 4),
+            "outputs_equal": True}
+        print(json.dumps({name: result["configs"][name]}), file=sys.stderr, flush=True)
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as f:
+        json.dump(result, f, indent=1)
+    print(json.dumps(result))
+
+
+if __name__ == "__main__":
+    main()
