@@ -219,42 +219,82 @@ def cpu_baseline_only(args, rank: int, world: int, cpu) -> None:
 
 
 def load_traffic_per_view():
-    """HBM bytes per view of the fused kernel from the committed rocprofv3 PMC summary
-    (profiles/pmc_main_kernel.json, written by tools/summarize_profile.py), if any."""
+    """The committed rocprofv3 PMC summary of the fused kernel on the C2 bench shape
+    (profiles/pmc_main_kernel.json: HBM bytes per view, reads from the gfx950 request-size
+    counters as calibrated by tools/fetch_probe.hip, writes from WRITE_SIZE), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_main_kernel.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_view")
+            d = json.load(f)
+        return d if d.get("hbm_bytes_per_view") else None
     except (OSError, ValueError):
         return None
 
 
-def segments_holding(mask, stride: int, frame_idx) -> int:
-    """64-byte segments of the given frames (frame f at byte f * stride of the stack) that hold a
-    valid pixel, summed over the frames: the pattern bytes a mask-first decode must read.  A lane's
-    8-byte load never straddles a segment (lanes start at multiples of 8 px, stride % 16 == 0).
-    `mask` is a flat torch bool tensor of the view's pixels."""
+def segments_holding(mask, stride: int, frame_idx, block: int = 64) -> int:
+    """Aligned ``block``-byte pieces (64-B segments, 128-B lines) of the given frames (frame f at
+    byte f * stride of the stack) that hold a valid pixel, summed over the frames: the pattern
+    bytes a mask-first decode must read at that granularity.  A lane's 8-byte load never straddles
+    one (lanes start at multiples of 8 px, stride % 16 == 0).  `mask` is a flat torch bool tensor
+    of the view's pixels."""
     import torch
+    shift = block.bit_length() - 1
     idx = torch.nonzero(mask.reshape(-1)).reshape(-1).to(torch.int64)
     total = 0
     for f in frame_idx:
-        total += int(torch.unique((idx + f * stride) >> 6).numel())
+        total += int(torch.unique((idx + f * stride) >> shift).numel())
     return total
 
 
-def mask_first_segments(frames, cfg, H, W, dev) -> int:
-    """`segments_holding` of one device view's pattern frames, its mask from the maps path."""
+def texture_lines_holding(mask, block: int = 128) -> int:
+    """``block``-byte pieces of the [n_px][3] texture that main3 reads: 24 bytes per 8-pixel lane
+    holding a valid pixel (mask first)."""
+    import torch
+    m = mask.reshape(-1)
+    n = m.numel()
+    pad = (-n) % 8
+    if pad:
+        m = torch.cat([m, torch.zeros(pad, dtype=m.dtype, device=m.device)])
+    lanes = torch.nonzero(m.reshape(-1, 8).any(1)).reshape(-1).to(torch.int64)
+    shift = block.bit_length() - 1
+    return int(torch.unique(torch.cat([(24 * lanes) >> shift, (24 * lanes + 23) >> shift])).numel())
+
+
+def _view_mask(frames, cfg, H, W, dev):
     from structured_light_for_3d_model_replication_amd import engine as E
-    rec = mask_first_segments.__dict__.setdefault("rec", {}).get((H, W))
+    rec = _view_mask.__dict__.setdefault("rec", {}).get((H, W))
     if rec is None:
-        rec = mask_first_segments.rec[(H, W)] = E.Reconstructor(H, W, device=dev)
-    _, _, mask = rec.decode(frames, cfg)
+        rec = _view_mask.rec[(H, W)] = E.Reconstructor(H, W, device=dev)
+    return rec.decode(frames, cfg)[2] != 0
+
+
+def mask_first_segments(frames, cfg, H, W, dev, block: int = 64) -> int:
+    """`segments_holding` of one device view's pattern frames, its mask from the maps path."""
+    mask = _view_mask(frames, cfg, H, W, dev)
     n = min(frames.n_frames, 2 + 2 * (cfg.n_sets_col + cfg.n_sets_row))   # frames the plan reads
-    if frames.stride % 64 == 0:          # every frame's segments line up: one count per frame
-        return (n - 2) * segments_holding(mask != 0, frames.stride, [0])
-    return segments_holding(mask != 0, frames.stride, range(2, n))
+    if frames.stride % block == 0:       # every frame's pieces line up: one count per frame
+        return (n - 2) * segments_holding(mask, frames.stride, [0], block)
+    return segments_holding(mask, frames.stride, range(2, n), block)
+
+
+def read_model(frames, cfg, H, W, dev, carried: bool = True) -> dict:
+    """The HBM bytes one view's fused launch reads, piece by piece, at the 128-byte request size
+    rocprofv3 shows for every main3 read (profiles/r4c/pmc_calibration.json: RDREQ_128B ~ all
+    requests; tools/fetch_probe.hip's mask-gated 8 B/lane reads fetch exactly the 128-B lines
+    holding a requested byte): white + black of every pixel, each pattern frame's lines holding a
+    valid pixel, the texture lines of valid lanes, and -- in the steady-state pipeline -- the
+    carried batch's white + black (Otsu partials)."""
+    mask = _view_mask(frames, cfg, H, W, dev)
+    n_px = H * W
+    dense = 2 * ((n_px + 127) // 128) * 128
+    out = {"white_black": dense,
+           "pattern_lines128": 128 * mask_first_segments(frames, cfg, H, W, dev, 128),
+           "texture_lines128": 128 * texture_lines_holding(mask, 128),
+           "carried_white_black": dense if carried else 0}
+    out["total"] = sum(out.values())
+    return out
 
 
 RESULT_OUT = sys.stdout          # main() points it at the original stdout
@@ -425,6 +465,7 @@ def main():
         pts += [int(clouds[0][k].count.item()) for k in range(B)]
     pts = pts[:P]
     seg_frames = [mask_first_segments(dframes[v], cfg, H, W, dev) for v in range(P)]
+    models = [read_model(dframes[v], cfg, H, W, dev, carried=args.pipeline in ("fused", "fused2")) for v in range(P)]
 
     K, Wm = args.steps, args.warmup
     # the whole run as ONE batch stream: warmup + timed + 2 look-ahead batches whose thresholds
@@ -549,13 +590,31 @@ def main():
         kern_avg_s = kern_sum / launches / 1e3
         achieved = dense_sum / launches / kern_avg_s / 1e9          # SURVEY 8(d)'s algorithmic bytes
         mf_achieved = bytes_sum / launches / kern_avg_s / 1e9       # the mask-first decode's own bytes
-        traffic_view = load_traffic_per_view() if args.config == "c2" else None
+        pmc = load_traffic_per_view() if args.config == "c2" else None
+        traffic_view = pmc["hbm_bytes_per_view"] if pmc else None
+        n_pts_mean = float(np.mean(pts))
+        model = {k: round(float(np.mean([m[k] for m in models]))) for k in models[0]}
+        model["writes"] = round(15 * n_pts_mean + 1024 * ((H * W + 4095) // 4096))   # cloud + Otsu partials
+        model["total_with_writes"] = model["total"] + model["writes"]
+        traffic_model = {"per_view": model,
+                         "what": "bytes the fused launch must move per view (pool average) at the 128-B read "
+                                 "request size the PMC counters show: white + black, pattern-frame lines holding a "
+                                 "valid pixel, texture lines of valid lanes, the carried batch's white + black; "
+                                 "writes 15 B per point (12 B XYZ + 3 B BGR) + 1 KB of Otsu partials per tile"}
+        if pmc:
+            traffic_model["measured_per_view"] = {"reads": pmc.get("fetch_bytes_per_view"),
+                                                  "writes": pmc.get("write_bytes_per_view"),
+                                                  "source": pmc.get("tag")}
+            traffic_model["measured_over_model"] = round(traffic_view / model["total_with_writes"], 4)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 # committed PMC bytes (profiles/pmc_main_kernel.json) are per C2 view
                 "traffic": round(traffic_view * B) if traffic_view else None,
-                "traffic_source": "profiles/pmc_main_kernel.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"
+                "traffic_source": ("profiles/pmc_main_kernel.json (rocprofv3 per launch: reads 128 x RDREQ_128B + "
+                                   "64 x RDREQ_64B + 32 x RDREQ_32B, = FETCH_SIZE x 2 since all reads are 128-B "
+                                   "requests, calibrated on known byte counts in profiles/r4c; writes WRITE_SIZE)")
                 if traffic_view else None,
+                "traffic_model": traffic_model,
                 "kernel": (f"main3_kernel<1,{int(f64)},1,1,false,PLAN=0x{(NC << 4) | NR:X}> (fused decode+triangulate+"
                            f"compaction, decode-plan instance, {B} views per launch)"
                            if (NC, NR) in ((11, 10), (11, 11), (12, 12)) else

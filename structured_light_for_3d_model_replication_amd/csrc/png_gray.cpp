@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <zlib.h>
+#include <emmintrin.h>
 
 #include <mutex>
 #include <vector>
@@ -137,27 +138,46 @@ bool inflate_all(const std::vector<uint8_t>& in, uint8_t* out, size_t n_out) {
   return ok;
 }
 
-inline int paeth(int a, int b, int c) {       // branch-free (selects), PNG spec §9.4
-  const int pa = abs(b - c), pb = abs(a - c), pc = abs(a + b - 2 * c);
-  const int bc = pb <= pc ? b : c;
-  return (pa <= pb && pa <= pc) ? a : bc;
+inline int iabs(int x) { const int m = x >> 31; return (x ^ m) - m; }
+
+inline int paeth(int a, int b, int c) {       // PNG spec §9.4, without branches: p - a = b - c,
+  const int db = b - c, da = a - c;           // p - b = a - c, p - c = (b - c) + (a - c)
+  const int pa = iabs(db), pb = iabs(da), pc = iabs(db + da);
+  const int m_bc = -int(pb <= pc), m_a = -int((pa <= pb) & (pa <= pc));   // masks, not branches:
+  const int bc = (b & m_bc) | (c & ~m_bc);                                 // the choice is data-
+  return (a & m_a) | (bc & ~m_a);                                          // random per pixel
+}
+
+// Sub filter of one row: out[x] = s[x] + out[x - 1] (mod 256), a byte-wise prefix sum -- 16
+// bytes per step (log-step shifts within the vector, then the carry of the previous block).
+void unfilter_sub(const uint8_t* __restrict s, uint8_t* __restrict d, uint32_t w) {
+  uint32_t x = 0;
+  __m128i carry = _mm_setzero_si128();
+  for (; x + 16 <= w; x += 16) {
+    __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + x));
+    v = _mm_add_epi8(v, _mm_slli_si128(v, 1));
+    v = _mm_add_epi8(v, _mm_slli_si128(v, 2));
+    v = _mm_add_epi8(v, _mm_slli_si128(v, 4));
+    v = _mm_add_epi8(v, _mm_slli_si128(v, 8));
+    v = _mm_add_epi8(v, carry);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(d + x), v);
+    carry = _mm_set1_epi8(char(d[x + 15]));
+  }
+  uint8_t a = x ? d[x - 1] : 0;
+  for (; x < w; ++x) d[x] = a = uint8_t(s[x] + a);
 }
 
 // Undo the row filters (1 byte per pixel) from raw [h][1 + w] into out [h][w].
 bool unfilter(const uint8_t* raw, uint8_t* out, uint32_t w, uint32_t h) {
   for (uint32_t y = 0; y < h; ++y) {
-    const uint8_t* s = raw + size_t(y) * (w + 1);
-    uint8_t* d = out + size_t(y) * w;
-    const uint8_t* up = y ? d - w : nullptr;
+    const uint8_t* __restrict s = raw + size_t(y) * (w + 1);
+    uint8_t* __restrict d = out + size_t(y) * w;
+    const uint8_t* __restrict up = y ? d - w : nullptr;
     const uint8_t f = s[0];
     ++s;
     switch (f) {
       case 0: memcpy(d, s, w); break;
-      case 1: {
-        uint8_t a = 0;
-        for (uint32_t x = 0; x < w; ++x) d[x] = a = uint8_t(s[x] + a);
-        break;
-      }
+      case 1: unfilter_sub(s, d, w); break;
       case 2:
         if (up) for (uint32_t x = 0; x < w; ++x) d[x] = uint8_t(s[x] + up[x]);
         else memcpy(d, s, w);
@@ -172,9 +192,10 @@ bool unfilter(const uint8_t* raw, uint8_t* out, uint32_t w, uint32_t h) {
         break;
       }
       case 4: {
+        if (!up) { unfilter_sub(s, d, w); break; }     // no prior row: Paeth predicts a (= Sub)
         int a = 0, c = 0;
         for (uint32_t x = 0; x < w; ++x) {
-          const int b = up ? up[x] : 0;
+          const int b = up[x];
           d[x] = uint8_t(s[x] + paeth(a, b, c));
           a = d[x];
           c = b;

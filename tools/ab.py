@@ -1,6 +1,9 @@
 #!/usr/bin/env python
-"""A/B of libslgpu.so builds on the benchmark's exact shape (C2, 12 views per fused launch,
-single-stream carried-histogram pipeline), one subprocess per variant, rounds interleaved.
+"""A/B of libslgpu.so builds on the benchmark's exact shape (C2, 16 views per fused launch,
+two-stream carried-histogram pipeline "fused2", a pool of 48 HBM views; --batch / --pipeline
+give round 2-3's 12-view one-stream shape), one subprocess per variant, rounds interleaved.
+The time is the step period: one HIP event pair around the timed launches, both streams joined
+(median_us = us per launch = per step).
 
     python tools/ab.py --libs build_ab/base.so,build_ab/w5b6.so [--rounds 3] [--launches 200]
 
@@ -41,38 +44,41 @@ def worker(a):
         os.replace(CACHE + ".tmp.npz", CACHE)
     cal = rig.tables()
     dev = torch.device("cuda", 0)
-    pool = [E.DeviceFrames(list(frames[i]), tex[i], device=dev) for _ in range(3) for i in range(12)]
+    B, NSL = a.batch, (4 if a.pipeline == "fused2" else 2)
+    pool = [E.DeviceFrames(list(frames[i]), tex[i], device=dev) for _ in range(4) for i in range(12)]
+    P = len(pool)
     dcal = E.DeviceCalib(cal, H, W, device=dev, tables=a.tables != "none", keep_table=a.tables == "rays")
     cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
-    B = 12
-    beng = E.BatchReconstructor(H, W, B, device=dev, slots=2)
-    clouds = [[E.Cloud(H * W, 1, False, device=dev) for _ in range(B)] for _ in range(2)]
+    beng = E.BatchReconstructor(H, W, B, device=dev, slots=NSL)
+    clouds = [[E.Cloud(H * W, 1, False, device=dev) for _ in range(B)] for _ in range(NSL)]
     preps = {}
 
     def prep(b):
-        key = (b % 3, b % 2)
+        key = ((b * B) % P, b % NSL)
         if key not in preps:
-            preps[key] = beng.prepare(pool[12 * (b % 3): 12 * (b % 3) + 12], cfg, dcal, clouds[b % 2], 1, 2.0, slot=b % 2)
+            preps[key] = beng.prepare([pool[(b * B + k) % P] for k in range(B)], cfg, dcal, clouds[b % NSL], 1, 2.0,
+                                      slot=b % NSL)
         return preps[key]
 
-    n = a.warmup + a.launches + 2
+    n = a.warmup + a.launches + NSL
     batches = [prep(b) for b in range(n)]
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.launches)]
-    for x, y in ev:
-        x.record()
-        y.record()
-    s = torch.cuda.Stream(device=dev)
+    s0, s1 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    beng.run_pipelined(batches, s, None, mode="fused", start=0, stop=a.warmup)
+    beng.run_pipelined(batches, s0, s1, mode=a.pipeline, start=0, stop=a.warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    beng.run_pipelined(batches, s, None, events=[(x.cuda_event, y.cuda_event) for x, y in ev], mode="fused",
-                       start=a.warmup, stop=a.warmup + a.launches)
+    e0.record(s0)
+    s1.wait_event(e0)
+    beng.run_pipelined(batches, s0, s1, mode=a.pipeline, start=a.warmup, stop=a.warmup + a.launches)
+    s0.wait_stream(s1)
+    e1.record(s0)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / a.launches * 1e6
-    us = sorted(x.elapsed_time(y) * 1e3 for x, y in ev)
+    step_us = e0.elapsed_time(e1) * 1e3 / a.launches
+    us = [step_us]
     last = a.warmup + a.launches - 1
-    cl = clouds[last % 2]
+    cl = clouds[last % NSL]
     counts = [int(c.count.item()) for c in cl]
     chk = float(sum(c.xyz[: int(c.count.item())].double().sum().item() for c in cl))
     err = int(np.frombuffer(beng.header(0, 0)[3084:3088].cpu().numpy().tobytes(), np.uint32)[0])
@@ -86,7 +92,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--libs", default="")
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--launches", type=int, default=200)
+    ap.add_argument("--launches", type=int, default=300)
+    ap.add_argument("--batch", type=int, default=16, help="views per fused launch (bench: 16)")
+    ap.add_argument("--pipeline", default="fused2", help="fused2 (bench: two streams) | fused (one stream)")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--tables", default="num", help="worker: num | none (DeviceCalib numerator tables) | rays (also the Nc ray table)")
@@ -108,7 +116,8 @@ def main():
             path, _, opt = spec.partition(":")
             if path:
                 env["SLG_LIB"] = path
-            cmd = [sys.executable, __file__, "--worker", "--launches", str(a.launches), "--warmup", str(a.warmup)]
+            cmd = [sys.executable, __file__, "--worker", "--launches", str(a.launches), "--warmup", str(a.warmup),
+                   "--batch", str(a.batch), "--pipeline", a.pipeline]
             if opt:
                 cmd += ["--tables", opt]
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout)
