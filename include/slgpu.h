@@ -277,6 +277,36 @@ int32_t slg_png_gray8_size(const char *path, int32_t *width, int32_t *height);
 int32_t slg_png_gray8_decode(const char *path, uint8_t *out, int64_t cap, int32_t width,
                              int32_t height);
 
+/* PNG decode on the device (the same cv2.imread of every used frame, for the batch file path):
+ * the host only reads the file and checks its chunks, the GPU inflates and un-filters.
+ * slg_png_zstream (host): for an 8-bit, non-interlaced PNG of colour type 0 (gray), 2 (RGB),
+ * 4 (gray + alpha) or 6 (RGBA), copies the concatenated IDAT payload (the zlib stream) into
+ * buf (cap bytes; needs zlen + 8, the file size + 8 always suffices) and fills info[4] =
+ * {width, height, channels, zlen}; returns 0, else non-zero (any other file, a CRC error, cap
+ * too small: decode it the general way).  Thread-safe.
+ * slg_png_decode_device: decodes n frames (DEVICE descriptors `frames`, each naming DEVICE
+ * buffers: z = the zlib stream as read by slg_png_zstream, 4-byte aligned and readable for
+ * zlen + 8 bytes; raw = scratch of slg_png_raw_bytes(w, h, ch) bytes; out = the samples,
+ * [height][out_pitch] rows of width * channels bytes).  status is DEVICE int32 [2 * n]:
+ * status[2f] = 0 or SLG_PNG_E_* (a frame with a non-zero status is left unspecified and must
+ * be decoded on the host), status[2f + 1] internal.  Asynchronous on `stream`; returns 0 or SLG_ERR_*. */
+#define SLG_PNG_E_STREAM 1     /* not a valid zlib/deflate stream (or reads past zlen) */
+#define SLG_PNG_E_SIZE 2       /* inflated size differs from height * (1 + width * channels) */
+#define SLG_PNG_E_ADLER 3      /* Adler-32 of the inflated bytes differs from the stream's */
+#define SLG_PNG_E_FILTER 4     /* a scanline filter type byte > 4 */
+#define SLG_PNG_E_UNSUPPORTED 5 /* rows wider than the device un-filter takes (width * channels > 24576) */
+typedef struct slg_png_frame {
+  const uint8_t *z;        /* zlib stream (device) */
+  int64_t zlen;
+  uint8_t *raw;            /* scratch (device), slg_png_raw_bytes() */
+  uint8_t *out;            /* samples (device) */
+  int64_t out_pitch;       /* bytes between output rows (>= width * channels) */
+  int32_t width, height, channels, reserved;
+} slg_png_frame;
+int32_t slg_png_zstream(const char *path, uint8_t *buf, int64_t cap, int32_t *info /* [4] */);
+int64_t slg_png_raw_bytes(int32_t width, int32_t height, int32_t channels);
+int32_t slg_png_decode_device(const slg_png_frame *frames, int32_t n, int32_t *status, void *stream);
+
 /* ---- Multi-GPU: the final point-cloud gather of a view-sharded scan.
  * Replaces nothing in the reference (its batch loop is serial, server/processing.py:314-334);
  * it is the one collective of the sharded path: after every rank has reconstructed its block

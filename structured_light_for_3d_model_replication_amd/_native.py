@@ -65,6 +65,14 @@ class Cloud(ctypes.Structure):
     _fields_ = [("xyz", c_vp), ("bgr", c_vp), ("count", c_vp), ("capacity", c_i64)]
 
 
+class PngFrame(ctypes.Structure):
+    _fields_ = [("z", c_vp), ("zlen", c_i64), ("raw", c_vp), ("out", c_vp), ("out_pitch", c_i64),
+                ("width", c_i32), ("height", c_i32), ("channels", c_i32), ("reserved", c_i32)]
+
+
+PNG_E_STREAM, PNG_E_SIZE, PNG_E_ADLER, PNG_E_FILTER, PNG_E_UNSUPPORTED = 1, 2, 3, 4, 5
+
+
 EXPORTS = {
     "slg_version": (c_i32, []),
     "slg_last_error": (ctypes.c_char_p, []),
@@ -105,6 +113,9 @@ EXPORTS = {
     "slg_ply_format": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "slg_png_gray8_size": (c_i32, [ctypes.c_char_p, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
     "slg_png_gray8_decode": (c_i32, [ctypes.c_char_p, c_vp, c_i64, c_i32, c_i32]),
+    "slg_png_zstream": (c_i32, [ctypes.c_char_p, c_vp, c_i64, ctypes.POINTER(c_i32)]),
+    "slg_png_raw_bytes": (c_i64, [c_i32, c_i32, c_i32]),
+    "slg_png_decode_device": (c_i32, [c_vp, c_i32, c_vp, c_vp]),
     "slg_rays_match_pinhole": (c_i32, [c_vp, c_i32, c_i32, c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_vp]),
     "slg_rgb_to_gray": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp]),
     "slg_gray_texture": (c_i32, [c_vp, c_i64, c_vp, c_vp]),

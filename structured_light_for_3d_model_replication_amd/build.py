@@ -8,7 +8,8 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "slgpu.hip")
-SRCS = [SRC, os.path.join(PKG, "csrc", "png_gray.cpp"), os.path.join(PKG, "csrc", "gather.cpp")]
+SRCS = [SRC, os.path.join(PKG, "csrc", "png_device.hip"), os.path.join(PKG, "csrc", "png_gray.cpp"),
+        os.path.join(PKG, "csrc", "gather.cpp")]
 HDR = os.path.join(ROOT, "include", "slgpu.h")
 OUT = os.path.join(PKG, "libslgpu.so")
 

@@ -38,12 +38,13 @@ bool read_file(const char* path, std::vector<uint8_t>& buf) {
 uint32_t chunk_crc(const uint8_t* p, size_t n);
 
 struct Png {
-  uint32_t w = 0, h = 0;
+  uint32_t w = 0, h = 0, ch = 1;
   std::vector<uint8_t> idat;                  // concatenated zlib stream
 };
 
-// Parse chunks; only 8-bit grayscale, compression 0, filter 0, no interlace is accepted.
-int parse(const std::vector<uint8_t>& b, Png& png, bool want_data) {
+// Parse chunks of an 8-bit, non-interlaced PNG (compression 0, filter 0) whose colour type is in
+// `types` (bit t set = colour type t accepted); png.ch = samples per pixel.
+int parse_types(const std::vector<uint8_t>& b, Png& png, bool want_data, uint32_t types) {
   static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0d, 0x0a, 0x1a, 0x0a};
   if (b.size() < 8 + 25 || memcmp(b.data(), sig, 8) != 0) return kInvalid;
   size_t o = 8;
@@ -60,7 +61,10 @@ int parse(const std::vector<uint8_t>& b, Png& png, bool want_data) {
       if (len != 13) return kInvalid;
       png.w = be32(data);
       png.h = be32(data + 4);
-      if (data[8] != 8 || data[9] != 0 || data[10] != 0 || data[11] != 0 || data[12] != 0) return kUnsupported;
+      const uint8_t ct = data[9];
+      if (data[8] != 8 || ct > 6 || !((types >> ct) & 1u) || data[10] != 0 || data[11] != 0 || data[12] != 0)
+        return kUnsupported;
+      png.ch = ct == 0 ? 1 : ct == 2 ? 3 : ct == 4 ? 2 : 4;
       if (png.w == 0 || png.h == 0 || png.w > (1u << 16) || png.h > (1u << 16)) return kUnsupported;
       have_hdr = true;
       if (!want_data) return kOk;
@@ -71,12 +75,15 @@ int parse(const std::vector<uint8_t>& b, Png& png, bool want_data) {
       have_end = true;
       break;
     } else if (critical) {
-      return kUnsupported;                     // PLTE etc.: not a grayscale capture
+      return kUnsupported;                     // PLTE etc.: not a capture this path decodes
     }
     o += 12 + size_t(len);
   }
   return have_hdr && have_end && !png.idat.empty() ? kOk : kInvalid;
 }
+
+// Only 8-bit grayscale (colour type 0).
+int parse(const std::vector<uint8_t>& b, Png& png, bool want_data) { return parse_types(b, png, want_data, 1u); }
 
 // libdeflate (optional): the three entry points of its stable public API.
 using ld_alloc_t = void* (*)();
@@ -239,6 +246,26 @@ int32_t slg_png_gray8_decode(const char* path, uint8_t* out, int64_t cap, int32_
   std::vector<uint8_t> raw(size_t(png.h) * (png.w + 1));
   if (!inflate_all(png.idat, raw.data(), raw.size())) return kInvalid;
   return unfilter(raw.data(), out, png.w, png.h) ? kOk : kInvalid;
+}
+
+// The zlib stream of an 8-bit gray / gray+alpha / RGB / RGBA PNG for the device decoder
+// (include/slgpu.h): the concatenated IDAT payload, 8 zero bytes of read-ahead padding after it.
+int32_t slg_png_zstream(const char* path, uint8_t* buf, int64_t cap, int32_t* info) {
+  if (!path || !buf || !info) return kInvalid;
+  std::vector<uint8_t> b;
+  if (!read_file(path, b)) return kInvalid;
+  Png png;
+  const int rc = parse_types(b, png, true, (1u << 0) | (1u << 2) | (1u << 4) | (1u << 6));
+  if (rc) return rc;
+  const int64_t n = int64_t(png.idat.size());
+  if (cap < n + 8) return kInvalid;
+  memcpy(buf, png.idat.data(), size_t(n));
+  memset(buf + n, 0, 8);
+  info[0] = int32_t(png.w);
+  info[1] = int32_t(png.h);
+  info[2] = int32_t(png.ch);
+  info[3] = int32_t(n);
+  return kOk;
 }
 
 }  // extern "C"

@@ -1798,15 +1798,16 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     for (int s = 0; s < NS; ++s) {
       // one lane per (round, wave) count: the tile aggregate and, for phase D, each (round,
       // wave)'s offset within the tile -- one wave-wide scan instead of per-round sums later
-      static_assert(kIt * (kB / 64) == 64, "one lane per (round, wave)");
-      const int cnt = (&s_cnt[s][0][0])[lane];
+      constexpr int kEnt = kIt * (kB / 64);           // 64 for 512-lane tiles, 32 for 256
+      static_assert(kEnt <= 64, "one lane per (round, wave)");
+      const int cnt = lane < kEnt ? (&s_cnt[s][0][0])[lane] : 0;
       int incl = cnt;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const int y = __shfl_up(incl, o);
         if (lane >= o) incl += y;
       }
-      (&s_loc[s][0][0])[lane] = incl - cnt;
+      if (lane < kEnt) (&s_loc[s][0][0])[lane] = incl - cnt;
       const int agg = __shfl(incl, 63);
       uint64_t* st = p.states + int64_t(s) * tiles;
       uint64_t excl;

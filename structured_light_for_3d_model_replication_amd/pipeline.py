@@ -76,6 +76,7 @@ class HostView:
     weights: int = N.GRAY_PNG       # rgb: libpng (PNG) or OpenCV (BMP) gray weights
     texture: torch.Tensor | None = None   # pinned [n_px, 3] BGR, or None: derived on the device
     pinned: list = field(default_factory=list)   # buffers to return to the pool
+    z: tuple | None = None          # kind "png_z": (frame indices, byte offsets, stream lengths)
 
 
 def _decode_rgb(path) -> np.ndarray:
@@ -89,13 +90,58 @@ def _decode_rgb(path) -> np.ndarray:
     return a
 
 
-def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", "png")) -> HostView:
-    """Discover + decode one capture into pinned memory (host work only; safe on any thread)."""
+def device_png_enabled() -> bool:
+    """PNG captures decoded on the GPU (``slg_png_decode_device``) with SLG_PNG_DEVICE=1; off by
+    default: the inflate is one wave per stream at ~0.5 s per 1080p frame, so even 16 views per
+    launch (704 streams) take 30 ms per view against 20 ms for the host decoder on the box's 16
+    CPUs (profiles/r4i).  Correct and tested (tests/test_png_device.py), kept for hosts with
+    fewer CPUs per GPU."""
+    return os.environ.get("SLG_PNG_DEVICE", "0") == "1" and not os.environ.get("SLG_PNG_PIL")
+
+
+def read_view_z(folder: str, files, need, pool: PinnedPool) -> HostView | None:
+    """Host half of the device PNG decode: the used frames' zlib streams (``slg_png_zstream``:
+    file read + chunk CRCs, no inflate) packed into one pinned buffer, 256-byte aligned each.
+    None when a used frame is not an 8-bit gray / RGB / RGBA PNG of one common size (the view is
+    then decoded on the host the general way)."""
+    if not all(files[i].lower().endswith(".png") for i in need):
+        return None
+    L = N.lib()
+    caps = [(os.path.getsize(files[i]) + 8 + 255) // 256 * 256 for i in need]
+    offs = [0]
+    for c in caps:
+        offs.append(offs[-1] + c)
+    buf = pool.get(offs[-1])
+    base = buf.data_ptr()
+    infos = [(ctypes.c_int32 * 4)() for _ in need]
+
+    def one(k):
+        return L.slg_png_zstream(os.fsencode(files[need[k]]), ctypes.c_void_p(base + offs[k]), caps[k], infos[k])
+    with ThreadPoolExecutor(max_workers=min(FR.decode_threads(), len(need))) as ex:
+        rcs = list(ex.map(one, range(len(need))))
+    shapes = {tuple(i[:3]) for i in infos}
+    if any(rcs) or len(shapes) != 1 or next(iter(shapes))[2] not in (1, 3, 4):
+        pool.put(buf)
+        return None
+    W, H, C = next(iter(shapes))
+    return HostView(folder, len(files), H, W, (H * W + 15) // 16 * 16, "png_z", buf, channels=C, pinned=[buf],
+                    z=(list(need), offs[:-1], [int(i[3]) for i in infos]))
+
+
+def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", "png"),
+              device_png: bool | None = None) -> HostView:
+    """Discover + read one capture into pinned memory (host work only; safe on any thread):
+    PNG captures as their zlib streams for the device decoder (``device_png``, default
+    :func:`device_png_enabled`), anything else decoded on the host."""
     from .processing import _needed_frames
     files = FR.discover(folder, order)
     if len(files) < 4:
         raise ValueError(f"Not enough images (got {len(files)}, need at least 4).")
     need = _needed_frames(len(files), cfg) if cfg.variant == "processing" else list(range(len(files)))
+    if device_png if device_png is not None else device_png_enabled():
+        hv = read_view_z(folder, files, need, pool)
+        if hv is not None:
+            return hv
     L = N.lib()
     w, h = ctypes.c_int32(), ctypes.c_int32()
     gray8 = (files[0].lower().endswith(".png") and not os.environ.get("SLG_PNG_PIL")
@@ -157,29 +203,92 @@ def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", 
                     weights=weights, pinned=[buf])
 
 
-def upload_view(hv: HostView, stream, need=None) -> E.DeviceFrames:
-    """Async H2D of a HostView on ``stream`` (pinned source) + the device texture: frame 0
+def upload_views(hvs, stream) -> list:
+    """Async H2D of HostViews on ``stream`` (pinned sources) + the device textures: frame 0
     replicated for gray captures, frame 0's BGR for colour ones (``slg_gray_texture`` /
-    ``slg_rgb_to_gray``).  The host buffers must stay alive until ``stream`` reaches here."""
-    dev = E.DeviceFrames.allocate(hv.n_files, hv.height, hv.width)
+    ``slg_rgb_to_gray``).  The PNG captures (kind "png_z") of the list are decoded by ONE
+    ``slg_png_decode_device`` launch over all their frames (a view's 44 streams alone leave the
+    GPU nearly idle: the decode is one wave per stream).  The host buffers must stay alive until
+    ``stream`` reaches here.  Returns the DeviceFrames in order."""
+    devs = [E.DeviceFrames.allocate(hv.n_files, hv.height, hv.width) for hv in hvs]
     sp = ctypes.c_void_p(stream.cuda_stream)
     L = N.lib()
     with torch.cuda.stream(stream):
-        if hv.kind == "gray":
-            dev.data[: hv.n_files].copy_(hv.stack, non_blocking=True)
-            if hv.texture is not None:
-                dev.texture.copy_(hv.texture, non_blocking=True)
-            else:
-                N.check(L.slg_gray_texture(ctypes.c_void_p(dev.data.data_ptr()), dev.n_px,
-                                           ctypes.c_void_p(dev.texture.data_ptr()), sp))
+        pngs = [(hv, dev) for hv, dev in zip(hvs, devs) if hv.kind == "png_z"]
+        if pngs:
+            decode_png_device(pngs, stream)
+        for hv, dev in zip(hvs, devs):
+            if hv.kind == "gray":
+                dev.data[: hv.n_files].copy_(hv.stack, non_blocking=True)
+                if hv.texture is not None:
+                    dev.texture.copy_(hv.texture, non_blocking=True)
+                else:
+                    N.check(L.slg_gray_texture(ctypes.c_void_p(dev.data.data_ptr()), dev.n_px,
+                                               ctypes.c_void_p(dev.texture.data_ptr()), sp))
+            elif hv.kind == "rgb":
+                rgb = torch.empty(hv.stack.shape, dtype=torch.uint8, device=dev.data.device)
+                rgb.copy_(hv.stack, non_blocking=True)
+                N.check(L.slg_rgb_to_gray(ctypes.c_void_p(rgb.data_ptr()), hv.channels, dev.n_px,
+                                          rgb.shape[1], hv.n_files, ctypes.c_void_p(dev.data.data_ptr()),
+                                          dev.stride, ctypes.c_void_p(dev.texture.data_ptr()), hv.weights, sp))
+                dev._rgb = rgb                          # keep the staging alive with the frames
+    return devs
+
+
+def upload_view(hv: HostView, stream) -> E.DeviceFrames:
+    """:func:`upload_views` of one view."""
+    return upload_views([hv], stream)[0]
+
+
+def decode_png_device(pngs, stream) -> None:
+    """Device half of the PNG decode for [(HostView "png_z", DeviceFrames)]: H2D of the zlib
+    streams, inflate + un-filter on the GPU (``slg_png_decode_device``, one launch for every
+    frame of every view) straight into the frame stacks (gray) or into RGB(A) staging stacks that
+    ``slg_rgb_to_gray`` converts, then the textures.  Enqueued on ``stream`` (current); each
+    view's ``dev._png_status`` (device int32 [2 * frames]) says whether the host must redo it."""
+    L = N.lib()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    device = pngs[0][1].data.device
+    n_all = sum(len(hv.z[0]) for hv, _ in pngs)
+    descs = (N.PngFrame * n_all)()
+    status = torch.zeros(2 * n_all, dtype=torch.int32, device=device)
+    keep, k0 = [], 0
+    for hv, dev in pngs:
+        need, offs, zlens = hv.z
+        n, C, n_px = len(need), hv.channels, hv.height * hv.width
+        zdev = torch.empty(hv.stack.numel(), dtype=torch.uint8, device=device)
+        zdev.copy_(hv.stack, non_blocking=True)
+        raw_b = int(L.slg_png_raw_bytes(hv.width, hv.height, C))
+        raw = torch.empty(n * raw_b, dtype=torch.uint8, device=device)
+        rgb = torch.empty((hv.n_files, n_px * C), dtype=torch.uint8, device=device) if C > 1 else None
+        for k, i in enumerate(need):
+            out = dev.data[i] if C == 1 else rgb[i]
+            descs[k0 + k] = N.PngFrame(z=zdev.data_ptr() + offs[k], zlen=zlens[k], raw=raw.data_ptr() + k * raw_b,
+                                       out=out.data_ptr(), out_pitch=hv.width * C, width=hv.width,
+                                       height=hv.height, channels=C, reserved=0)
+        dev._png_status = status[2 * k0: 2 * (k0 + n)]
+        dev._png_keep = (zdev, raw, rgb)                 # alive until the view is collected
+        keep.append((hv, dev, rgb))
+        k0 += n
+    dbytes = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(descs), ctypes.sizeof(descs))),
+                              dtype=torch.uint8).pin_memory()
+    ddev = dbytes.to(device, non_blocking=True)
+    N.check(L.slg_png_decode_device(ctypes.c_void_p(ddev.data_ptr()), n_all, ctypes.c_void_p(status.data_ptr()), sp))
+    for hv, dev, rgb in keep:
+        if rgb is None:
+            N.check(L.slg_gray_texture(ctypes.c_void_p(dev.data.data_ptr()), dev.n_px,
+                                       ctypes.c_void_p(dev.texture.data_ptr()), sp))
         else:
-            rgb = torch.empty(hv.stack.shape, dtype=torch.uint8, device=dev.data.device)
-            rgb.copy_(hv.stack, non_blocking=True)
-            N.check(L.slg_rgb_to_gray(ctypes.c_void_p(rgb.data_ptr()), hv.channels, dev.n_px,
-                                      rgb.shape[1], hv.n_files, ctypes.c_void_p(dev.data.data_ptr()),
-                                      dev.stride, ctypes.c_void_p(dev.texture.data_ptr()), hv.weights, sp))
-            dev._rgb = rgb                              # keep the staging alive with the frames
-    return dev
+            N.check(L.slg_rgb_to_gray(ctypes.c_void_p(rgb.data_ptr()), hv.channels, dev.n_px, rgb.shape[1],
+                                      hv.n_files, ctypes.c_void_p(dev.data.data_ptr()), dev.stride,
+                                      ctypes.c_void_p(dev.texture.data_ptr()), N.GRAY_PNG, sp))
+        dev._png_desc = (dbytes, ddev)                   # the descriptors, until the launch ran
+
+
+def png_failed(dev: E.DeviceFrames) -> bool:
+    """Whether any frame of a device-decoded capture needs the host decoder (call after sync)."""
+    st = getattr(dev, "_png_status", None)
+    return st is not None and bool((st.view(-1, 2)[:, 0] != 0).any().item())
 
 
 @dataclass
@@ -252,14 +361,23 @@ class BatchPipeline:
     # ---- stages
     def _launch(self, g: _Group):
         """Upload g's views (copy stream) and launch their reconstruction (compute stream)."""
+        got = []
         for k, (folder, fut) in enumerate(g.entries):
             if fut is None:
                 continue
             try:
-                hv = fut.result()
-                g.views.append((k, hv, upload_view(hv, self.copy_stream)))
+                got.append((k, fut.result()))
             except Exception as e:  # noqa: BLE001 - per-folder isolation like the reference
                 g.errors[k] = e
+        try:                                           # one upload (one PNG decode launch) per group
+            devs = upload_views([hv for _, hv in got], self.copy_stream) if got else []
+            g.views += [(k, hv, d) for (k, hv), d in zip(got, devs)]
+        except Exception:  # noqa: BLE001 - then view by view, so the failure stays with its folder
+            for k, hv in got:
+                try:
+                    g.views.append((k, hv, upload_view(hv, self.copy_stream)))
+                except Exception as e:  # noqa: BLE001
+                    g.errors[k] = e
         if not g.views:
             return
         ev = torch.cuda.Event()
@@ -287,8 +405,26 @@ class BatchPipeline:
         if not g.views:
             return res
         g.event.synchronize()
+        from .processing import reconstruct_view
+        redo = {k for k, _, dev in g.views if png_failed(dev)}
+        for k, hv, dev in g.views:               # a frame the device decoder refused: the host decodes
+            if k in redo:                        # the whole view again (general path) and runs it alone
+                try:
+                    hv2 = read_view(hv.folder, self.cfg, self.pool, self.order, device_png=False)
+                    try:
+                        dev2 = upload_view(hv2, self.copy_stream)
+                        self.copy_stream.synchronize()
+                        (_, _), dc = self._engine(dev2.height, dev2.width)
+                        res[k] = reconstruct_view(dev2, self.cfg, self.calib, self.row_mode, self.tol, dc=dc)
+                    finally:
+                        for t in hv2.pinned:
+                            self.pool.put(t)
+                except Exception as e:  # noqa: BLE001
+                    res[k] = e
         if g.batch is not None:
             for (k, hv, _), c in zip(g.views, g.clouds):
+                if k in redo:
+                    continue
                 n = int(c.count.item())
                 body = self.formatter.body(c.xyz[:n], c.bgr[:n], self.format_stream) if self.device_ply else None
                 if body is None:                        # host formatting (or a value it must print)
@@ -298,8 +434,9 @@ class BatchPipeline:
                     host[: body.numel()].copy_(body)
                     res[k] = FormattedCloud(n, host, body.numel(), self.pool)
         else:                                       # isolate the failing view(s)
-            from .processing import reconstruct_view
             for k, hv, dev in g.views:
+                if k in redo:
+                    continue
                 try:
                     (_, _), dc = self._engine(dev.height, dev.width)
                     res[k] = reconstruct_view(dev, self.cfg, self.calib, self.row_mode, self.tol, dc=dc)

@@ -3,8 +3,10 @@
 of 8-bit PNG captures (PNG decode on a host thread pool with the next folder prefetched, H2D,
 fused kernels, native ASCII PLY writer).  Reported in DESIGN.md, never the bench metric.
 
-Prints one JSON line: seconds per view for the whole batch, and the serial cost of its parts
-(frame read + decode, reconstruct incl. H2D/D2H, PLY write) measured view by view.
+Prints one JSON line: seconds per view for the whole batch with the PNGs decoded on the GPU
+(``slg_png_decode_device``: host reads files only) and on host threads, and the serial cost of
+the parts (frame read [+ host decode], H2D [+ device decode] + kernels + D2H, PLY write) measured
+view by view; and whether both decoders gave the same PLY bytes.
 """
 from __future__ import annotations
 
@@ -22,7 +24,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--views", type=int, default=16)
-    ap.add_argument("--groups", type=int, nargs="+", default=[1, 8])
+    ap.add_argument("--groups", type=int, nargs="+", default=[1, 4])
     args = ap.parse_args()
 
     from structured_light_for_3d_model_replication_amd import calibration, synth
@@ -39,12 +41,15 @@ def main():
         folders = sorted(os.path.join(root, d) for d in os.listdir(root))
         kw = dict(n_sets_col=11, n_sets_row=10)
         PR.ProcessingLogic.process_multi_ply(calib, folders[0], "single", log_callback=lambda m: None, **kw)  # warm-up
-        batch_s = {}
-        for g in args.groups:                        # views per batched launch (SLG_BATCH_VIEWS)
-            os.environ["SLG_BATCH_VIEWS"] = str(g)
-            t0 = time.perf_counter()
-            PR.ProcessingLogic.process_multi_ply(calib, root, "batch", log_callback=lambda m: None, **kw)
-            batch_s[g] = round((time.perf_counter() - t0) / args.views, 4)
+        batch_s, plys = {}, {}
+        for dec in ("device", "host"):                # PNG inflate + un-filter on the GPU, or host threads
+            os.environ["SLG_PNG_DEVICE"] = "1" if dec == "device" else "0"
+            for g in args.groups:                     # views per batched launch (SLG_BATCH_VIEWS)
+                os.environ["SLG_BATCH_VIEWS"] = str(g)
+                t0 = time.perf_counter()
+                PR.ProcessingLogic.process_multi_ply(calib, root, "batch", log_callback=lambda m: None, **kw)
+                batch_s[f"{dec}_png_group{g}"] = round((time.perf_counter() - t0) / args.views, 4)
+            plys[dec] = [open(os.path.join(f, os.path.basename(f) + ".ply"), "rb").read() for f in folders]
 
         # the pipeline's stages one view at a time, serially (what the overlap hides)
         import torch
@@ -53,25 +58,28 @@ def main():
         cal = calibration.load_mat(calib)
         pool = PL.PinnedPool()
         s = torch.cuda.Stream()
-        t_read = t_rec = t_ply = 0.0
+        parts = {}
         pts = 0
-        for f in folders:
-            t = time.perf_counter(); hv = PL.read_view(f, cfg, pool); t_read += time.perf_counter() - t
-            t = time.perf_counter()
-            dev = PL.upload_view(hv, s)
-            s.synchronize()
-            P, C = PR.reconstruct_view(dev, cfg, cal, 1, 2.0)
-            t_rec += time.perf_counter() - t
-            for b in hv.pinned:
-                pool.put(b)
-            t = time.perf_counter(); PR.ProcessingLogic._save_ply(P, C, os.path.join(tmp, "x.ply")); t_ply += time.perf_counter() - t
-            pts += len(P)
-        n = len(folders)
+        for dec in ("device", "host"):
+            t_read = t_rec = t_ply = 0.0
+            for f in folders:
+                t = time.perf_counter(); hv = PL.read_view(f, cfg, pool, device_png=dec == "device"); t_read += time.perf_counter() - t
+                t = time.perf_counter()
+                dev = PL.upload_view(hv, s)
+                s.synchronize()
+                P, C = PR.reconstruct_view(dev, cfg, cal, 1, 2.0)
+                t_rec += time.perf_counter() - t
+                for b in hv.pinned:
+                    pool.put(b)
+                t = time.perf_counter(); PR.ProcessingLogic._save_ply(P, C, os.path.join(tmp, "x.ply")); t_ply += time.perf_counter() - t
+                pts += len(P)
+            n = len(folders)
+            parts[dec] = {"read_pinned": round(t_read / n, 4), "h2d_decode_kernels_d2h": round(t_rec / n, 4),
+                          "ply_write": round(t_ply / n, 4)}
         print(json.dumps({"what": "process_multi_ply batch, C2 PNG folders (end to end)", "views": n,
-                          "points_per_view": pts // n, "s_per_view_batch_by_group": batch_s,
-                          "s_per_view_parts": {"read_decode_png_pinned": round(t_read / n, 4),
-                                               "h2d_kernels_d2h": round(t_rec / n, 4),
-                                               "ply_write": round(t_ply / n, 4)},
+                          "points_per_view": pts // (2 * n), "s_per_view_batch": batch_s,
+                          "s_per_view_parts_serial": parts,
+                          "ply_bytes_device_equal_host": plys["device"] == plys["host"],
                           "decode_threads": PR.FR.decode_threads(), "host_cpus": os.cpu_count()}), flush=True)
 
 
