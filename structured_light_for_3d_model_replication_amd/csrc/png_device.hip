@@ -54,14 +54,24 @@ struct Huff {
   uint16_t sym[288];
 };
 
+constexpr uint32_t kRsrcFlags = 0x00020000;  // buffer descriptor word 3 (as the frame loads use)
+
 __device__ inline uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// A buffer descriptor over [p, p + n) built from wave-uniform (SGPR) values: the frame
+// descriptor is a per-workgroup load the compiler cannot prove uniform, and a descriptor left in
+// VGPRs turns every buffer access into a readfirstlane waterfall loop.
+__device__ inline __amdgpu_buffer_rsrc_t uni_rsrc(const void* p, uint32_t n) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint64_t u = uint64_t(uni(uint32_t(a))) | (uint64_t(uni(uint32_t(a >> 32))) << 32);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(u), 0, uni(n), kRsrcFlags);
+}
 
 // Wave-uniform LSB-first bit reader over the zlib stream.  The stream arrives 256 bytes at a time
 // by ONE vector buffer load (lane i holds word i of the chunk) issued a chunk ahead, and a refill
 // takes the next word with v_readlane (an SGPR): no load sits on the decode's critical path, and
 // no flat access whose completion every LDS wait (lgkmcnt) would also have to await.  Reads past
 // the stream come back 0 (buffer bounds).
-constexpr uint32_t kRsrcFlags = 0x00020000;  // buffer descriptor word 3 (as the frame loads use)
 
 struct Bits {
   __amdgpu_buffer_rsrc_t rsrc;
@@ -73,7 +83,7 @@ struct Bits {
 };
 
 __device__ inline void bits_init(Bits& b, const uint8_t* z, int64_t zlen) {
-  b.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(z), 0, uint32_t(zlen), kRsrcFlags);
+  b.rsrc = uni_rsrc(z, uint32_t(zlen));
   const int lane = threadIdx.x;
   b.cur = __builtin_amdgcn_raw_buffer_load_b32(b.rsrc, lane * 4, 0, 0);
   b.next = __builtin_amdgcn_raw_buffer_load_b32(b.rsrc, lane * 4, 256, 0);
@@ -92,6 +102,7 @@ __device__ inline void refill(Bits& b) {
       b.cur = b.next;
       b.base += 256;
       b.k = 0;
+      __builtin_amdgcn_sched_barrier(0);                 // (so the load may land in `next` itself)
       b.next = __builtin_amdgcn_raw_buffer_load_b32(b.rsrc, int(threadIdx.x) * 4, int(b.base + 256), 0);
     }
   }
@@ -107,35 +118,42 @@ __device__ inline uint32_t getbits(Bits& b, int n) {        // n <= 16
   return v;
 }
 
-__device__ inline int decode(Bits& b, const Huff& h) {
-  refill(b);
-  const uint32_t e = uni(h.fast[uint32_t(b.buf) & ((1u << kFastBits) - 1u)]);
-  if (e >> 9) {
-    const int len = int(e >> 9);
-    b.buf >>= len;
-    b.cnt -= len;
-    return int(e & 511u);
-  }
-  int code = 0, first = 0, index = 0;                        // canonical decode, a bit at a time
-  for (int len = 1; len <= 15; ++len) {                      // (cnt > 32 - 15 bits after refill)
-    code |= int(b.buf & 1u);
-    b.buf >>= 1;
-    --b.cnt;
-    const int count = int(uni(h.count[len]));
-    if (code - count < first) return int(uni(h.sym[index + (code - first)]));
+// Codes longer than kFastBits: canonical decode a bit at a time (rare; kept out of line so the
+// decode loop stays small).  Returns symbol | bits << 16, or ~0u for an invalid code.  Takes and
+// returns plain values: the caller re-reads the result with readfirstlane, so the symbol stays
+// wave-uniform (SGPRs, scalar branches) on both paths.
+__device__ __attribute__((noinline)) uint32_t decode_slow(uint64_t buf, const Huff& h) {
+  int code = 0, first = 0, index = 0;
+#pragma unroll 1
+  for (int len = 1; len <= 15; ++len) {
+    code |= int(buf & 1u);
+    buf >>= 1;
+    const int count = int(h.count[len]);
+    if (code - count < first) return uint32_t(h.sym[index + (code - first)]) | (uint32_t(len) << 16);
     index += count;
     first += count;
     first <<= 1;
     code <<= 1;
   }
-  return -1;
+  return ~0u;
+}
+
+__device__ inline int decode(Bits& b, const Huff& h) {
+  refill(b);                                                 // (cnt > 32 >= 15 bits after it)
+  const uint32_t e = uni(h.fast[uint32_t(b.buf) & ((1u << kFastBits) - 1u)]);
+  const uint32_t r = (e >> 9) ? ((e & 511u) | ((e >> 9) << 16)) : uni(decode_slow(b.buf, h));
+  if (r == ~0u) return -1;
+  const int len = int(r >> 16);
+  b.buf >>= len;
+  b.cnt -= len;
+  return int(r & 0xffffu);
 }
 
 // Build `h` from code lengths lens[0..n) (LDS); all 64 lanes call it.  False for an
 // over-subscribed set (an incomplete one decodes only its codes: a missing code fails decode()).
 // w: LDS work words [48] (start of each length in the sorted symbols, its first canonical code,
 // a running cursor).
-__device__ bool build(Huff& h, const uint8_t* lens, int n, uint32_t* w) {
+__device__ __attribute__((noinline)) bool build(Huff& h, const uint8_t* lens, int n, uint32_t* w) {
   const int lane = threadIdx.x;
   uint32_t* offs = w;
   uint32_t* first = w + 16;
@@ -216,7 +234,7 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
   const int64_t n_out = int64_t(f.height) * row;
   Bits b;
   bits_init(b, f.z, f.zlen);
-  const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(f.raw, 0, uint32_t(n_out), kRsrcFlags);
+  const __amdgpu_buffer_rsrc_t out = uni_rsrc(f.raw, uint32_t(n_out));
   int err = 0;
   int64_t pos = 0, flushed = 0;
   int ridx = 0;                                            // pos % kRing
@@ -267,7 +285,7 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
       }
       if (lane < 19) L.lens[lane] = uint8_t(cl[lane]);
       __syncthreads();
-      if (!build(L.dist, L.lens, 19, L.work)) { err = SLG_PNG_E_STREAM; break; }   // code-length code
+      if (!uni(build(L.dist, L.lens, 19, L.work))) { err = SLG_PNG_E_STREAM; break; }   // code-length code
       // the HLIT + HDIST code lengths (wave-uniform), written over the code-length code's own
       // lengths (no longer needed: its table is built) -- litlen at [0, hlit), distance at 288
       int i = 0;
@@ -298,7 +316,7 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
       __syncthreads();
       if (L.lens[256] == 0) { err = SLG_PNG_E_STREAM; break; }
     }
-    if (!build(L.lit, L.lens, hlit, L.work) || !build(L.dist, L.lens + 288, hdist, L.work)) {
+    if (!uni(build(L.lit, L.lens, hlit, L.work)) || !uni(build(L.dist, L.lens + 288, hdist, L.work))) {
       err = SLG_PNG_E_STREAM;
       break;
     }

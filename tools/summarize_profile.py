@@ -85,7 +85,9 @@ def main():
 
     # PMC: HBM bytes per view
     out = {"source": f"gpurun_out/{a.tag}", "kernel": a.kernel,
-           "units": "bytes; FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read correction), WRITE_SIZE KiB x 1024"}
+           "units": "bytes; reads 128 x RDREQ_128B + 64 x RDREQ_64B + 32 x RDREQ_32B (calibrated on known "
+                    "byte counts, profiles/r4c; = FETCH_SIZE KiB x 1024 x 2 when all reads are 128-B requests), "
+                    "WRITE_SIZE KiB x 1024"}
     per = {}
     for pmc, key, scale in (("fetch", "FETCH_SIZE", 2048), ("write", "WRITE_SIZE", 1024)):
         rows = rows_of(os.path.join(src, pmc, f"{pmc}_counter_collection.csv"), a.kernel)
@@ -95,6 +97,17 @@ def main():
             per[key] = sum(float(r["Counter_Value"]) * scale for r in rows) / views
             out[key.lower() + "_bytes_per_view"] = round(per[key])
             out[key.lower() + "_launches"] = len(rows)
+    rr = rows_of(os.path.join(src, "rdreq", "rdreq_counter_collection.csv"), a.kernel)
+    if rr:                                   # the request-size reading of the reads (validated)
+        byc = collections.defaultdict(float)
+        views = sum(vof(int(r["Grid_Size"])) for r in rr if r["Counter_Name"] == "TCC_EA0_RDREQ_sum")
+        for r in rr:
+            byc[r["Counter_Name"]] += float(r["Counter_Value"])
+        rd = (32 * byc["TCC_EA0_RDREQ_32B_sum"] + 64 * byc["TCC_EA0_RDREQ_64B_sum"]
+              + 128 * byc["TCC_EA0_RDREQ_128B_sum"]) / max(1, views)
+        out["rdreq_bytes_per_view"] = round(rd)
+        out["rdreq_128B_share"] = round(byc["TCC_EA0_RDREQ_128B_sum"] / max(1.0, byc["TCC_EA0_RDREQ_sum"]), 4)
+        per["FETCH_SIZE"] = rd                       # the validated formula replaces FETCH_SIZE x 2
     if per:
         out["hbm_bytes_per_view"] = round(sum(per.values()))
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
@@ -102,8 +115,9 @@ def main():
     if per and not a.no_refresh:
         with open(os.path.join(ROOT, "profiles", "pmc_main_kernel.json"), "w") as f:
             json.dump({"tag": a.tag, "kernel": a.kernel, "hbm_bytes_per_view": out["hbm_bytes_per_view"],
-                       "fetch_bytes_per_view": out.get("fetch_size_bytes_per_view"),
-                       "write_bytes_per_view": out.get("write_size_bytes_per_view")}, f, indent=1)
+                       "fetch_bytes_per_view": round(per["FETCH_SIZE"]) if "FETCH_SIZE" in per else None,
+                       "write_bytes_per_view": out.get("write_size_bytes_per_view"),
+                       "formula": out["units"]}, f, indent=1)
     print(json.dumps({"trace": res, "pmc": out}, indent=1))
 
 
