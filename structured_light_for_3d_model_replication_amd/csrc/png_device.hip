@@ -149,6 +149,42 @@ __device__ inline int decode(Bits& b, const Huff& h) {
   return int(r & 0xffffu);
 }
 
+// The primary table of a built code held in VGPRs (PNG_VTAB): entry pair d (entries 2d, 2d + 1)
+// in lane d % 64 of word d / 64.  A lookup is one indexed v_readlane into an SGPR, a few cycles,
+// where the LDS table costs an LDS round trip (~100 cycles) on the serial chain of every symbol.
+#ifndef PNG_VTAB
+#define PNG_VTAB 1
+#endif
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+static_assert((1 << kFastBits) / 128 == 8, "eight table words per lane");
+struct VTab {
+  u32x8 w;
+};
+
+__device__ inline void vtab_load(VTab& t, const Huff& h) {
+  const uint32_t* f = reinterpret_cast<const uint32_t*>(h.fast);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) t.w[r] = f[r * 64 + int(threadIdx.x)];
+}
+
+__device__ inline int decode(Bits& b, const VTab& t, const Huff& h) {
+  refill(b);
+  const uint32_t idx = uint32_t(b.buf) & ((1u << kFastBits) - 1u);
+  const uint32_t d = idx >> 1;
+  // lane d % 64 of all eight words (independent readlanes, pipelined) into SGPRs, then word d / 64
+  u32x8 sw;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) sw[r] = __builtin_amdgcn_readlane(t.w[r], int(d & 63u));
+  const uint32_t pair = sw[d >> 6];
+  const uint32_t e = (pair >> ((idx & 1u) * 16u)) & 0xffffu;
+  const uint32_t r = (e >> 9) ? ((e & 511u) | ((e >> 9) << 16)) : uni(decode_slow(b.buf, h));
+  if (r == ~0u) return -1;
+  const int len = int(r >> 16);
+  b.buf >>= len;
+  b.cnt -= len;
+  return int(r & 0xffffu);
+}
+
 // Build `h` from code lengths lens[0..n) (LDS); all 64 lanes call it.  False for an
 // over-subscribed set (an incomplete one decodes only its codes: a missing code fails decode()).
 // w: LDS work words [48] (start of each length in the sorted symbols, its first canonical code,
@@ -320,8 +356,18 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
       err = SLG_PNG_E_STREAM;
       break;
     }
+#if PNG_VTAB
+    VTab vlit, vdist;
+    vtab_load(vlit, L.lit);
+    vtab_load(vdist, L.dist);
+#define PNG_LIT vlit, L.lit
+#define PNG_DIST vdist, L.dist
+#else
+#define PNG_LIT L.lit
+#define PNG_DIST L.dist
+#endif
     for (;;) {                                               // the block's symbols
-      int s = decode(b, L.lit);
+      int s = decode(b, PNG_LIT);
       if (s < 0) { err = SLG_PNG_E_STREAM; break; }
       if (s < 256) {
         if (pos >= n_out) { err = SLG_PNG_E_SIZE; break; }
@@ -332,7 +378,7 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
       s -= 257;
       if (s >= 29) { err = SLG_PNG_E_STREAM; break; }
       const int len = int(kLenBase[s]) + int(getbits(b, kLenExtra[s]));
-      const int ds = decode(b, L.dist);
+      const int ds = decode(b, PNG_DIST);
       if (ds < 0 || ds >= 30) { err = SLG_PNG_E_STREAM; break; }
       const int dist = int(kDistBase[ds]) + int(getbits(b, kDistExtra[ds]));
       if (dist > pos) { err = SLG_PNG_E_STREAM; break; }

@@ -1543,6 +1543,41 @@ constexpr int kItemSlots = kTilePx + (kTilePx >> SLG_ITEM_PAD), kBgrSlots = kTil
 __device__ inline int item_slot(int m) { return m + (m >> SLG_ITEM_PAD); }
 __device__ inline int bgr_slot(int m) { return m + (m >> SLG_BGR_PAD); }
 
+// Phase D's BGR output: 3 bytes per kept point, so a lane's own stores are a 2-byte and a 1-byte
+// store at odd addresses (16 per lane per tile).  Staged instead: each kept point's 24-bit colour
+// goes to LDS word l (its index within the tile's kept points), and the workgroup writes the
+// tile's contiguous byte range [3 base, 3 (base + agg)) as 16-byte aligned stores, each lane
+// packing six staged words into four output dwords; the two ragged end chunks go byte by byte.
+#ifndef SLG_BGR_STAGE
+#define SLG_BGR_STAGE 1
+#endif
+constexpr int kStageWords = kTilePx + 8;          // + the 6-word read window past the last point
+
+__device__ inline void bgr_tile_store(uint8_t* gb, int64_t base, int agg, const uint32_t* w) {
+  const uint64_t start = reinterpret_cast<uint64_t>(gb) + uint64_t(3 * base);
+  const int a0 = int(start & 15u);
+  uint8_t* g = reinterpret_cast<uint8_t*>(start - uint64_t(a0));
+  const int nb = 3 * agg;                         // the tile's BGR bytes
+  const int nch = (a0 + nb + 15) >> 4;
+  for (int c = int(threadIdx.x); c < nch; c += kTileBlock) {
+    const int lo = c << 4, j0 = lo - a0;          // chunk start: in g, in the tile's byte stream
+    if (j0 >= 0 && j0 + 16 <= nb) {
+      const int l0 = j0 / 3, k0 = j0 - 3 * l0;
+      const uint32_t x0 = w[l0], x1 = w[l0 + 1], x2 = w[l0 + 2], x3 = w[l0 + 3], x4 = w[l0 + 4], x5 = w[l0 + 5];
+      const uint32_t q0 = x0 | (x1 << 24), q1 = (x1 >> 8) | (x2 << 16), q2 = (x2 >> 16) | (x3 << 8),
+                     q3 = x4 | (x5 << 24), q4 = x5 >> 8;   // the 18 stream bytes from point l0 on
+      const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(q1, q0, k0), __builtin_amdgcn_alignbyte(q2, q1, k0),
+                                 __builtin_amdgcn_alignbyte(q3, q2, k0), __builtin_amdgcn_alignbyte(q4, q3, k0));
+      *reinterpret_cast<uint4*>(g + lo) = v;
+    } else {
+      for (int t = 0; t < 16; ++t) {
+        const int j = j0 + t;
+        if (j >= 0 && j < nb) g[lo + t] = uint8_t(w[j / 3] >> (8 * (j % 3)));
+      }
+    }
+  }
+}
+
 // Phase B of main3 for rounds [i, i + G) (item m = tid + 256 * round), FAST path: the G items'
 // loads and fp64 chains are independent, so their plane gathers are in flight together.
 // tri_rounds: i is a compile-time multiple of G (the unrolled group loop); tri_rounds_at: any i.
@@ -1608,6 +1643,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   __shared__ int s_cnt[NS][kIt][kB / 64];  // kept points per (round, wave)
   __shared__ int s_loc[NS][kIt][kB / 64];  // their exclusive offsets within the tile (phase C)
   __shared__ uint64_t s_excl[NS];
+  __shared__ int s_agg[NS];                // kept points of the tile (phase C)
   // the carried batch's nibble planes and histograms in LDS of their own (68 KB per workgroup,
   // two per CU): each wave stages its lane data as soon as phase A ends, no extra barrier
   // (289.7 vs 291.6 us per launch against aliasing the item arrays after phase B)
@@ -1824,6 +1860,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       }
       if (lane == 0) {
         s_excl[s] = excl;
+        s_agg[s] = agg;
         if (tail) {
           p.ws->totals[s] = int64_t(excl) + agg;
           if (ROW_MODE != 2) *p.count = int64_t(excl) + agg;
@@ -1840,6 +1877,9 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // ------------------------------------------------------------ D: ordered stores from registers
   if (PROF && (p.dbg & 4)) return;                   // ablation: no output stores
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  // BGR staging words (SLG_BGR_STAGE) alias the item array: its last reader was phase B
+  static_assert(NS * kStageWords * 4 <= kItemSlots * 8, "BGR staging fits the item array");
+  uint32_t* s_stage = reinterpret_cast<uint32_t*>(s_item);
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int64_t base = int64_t(s_excl[s]);
@@ -1848,16 +1888,26 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
 #pragma unroll
     for (int i = 0; i < kIt; ++i) {
       if ((km[s][i] >> lane) & 1ull) {
-        const int64_t q = base + s_loc[s][i][wave] + __popcll(km[s][i] & lt);
+        const int l = s_loc[s][i][wave] + __popcll(km[s][i] & lt);
+        const int64_t q = base + l;
         const uint32_t c = s_bgr[bgr_slot(tid + kB * i)];
         if (!(PROF && (p.dbg & 128))) {              // PROF ablation bit 7: no XYZ stores
           gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
         }
-        if (!(PROF && (p.dbg & 8))) {                // PROF ablation bit 3: no BGR stores
+        if (SLG_BGR_STAGE) {
+          s_stage[s * kStageWords + l] = c;
+        } else if (!(PROF && (p.dbg & 8))) {         // PROF ablation bit 3: no BGR stores
           gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
         }
       }
     }
+  }
+  if (SLG_BGR_STAGE) {
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (!(PROF && (p.dbg & 8)))
+        bgr_tile_store(s == 0 ? p.bgr : p.scratch_bgr, int64_t(s_excl[s]), s_agg[s], s_stage + s * kStageWords);
   }
   if (prof) {
     __syncthreads();

@@ -11,7 +11,7 @@ for spec in "$@"; do
   flags=${spec#*:}
   [ "$name" = "$spec" ] && flags=""
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -mllvm -amdgpu-sched-strategy=max-ilp -fPIC -shared $flags \
-    -o "$R/build_ab/$name.so" "$P/slgpu.hip" "$P/png_gray.cpp" "$P/gather.cpp" -lz -ldl > "$R/build_ab/$name.log" 2>&1 &
+    -o "$R/build_ab/$name.so" "$P/slgpu.hip" "$P/png_device.hip" "$P/png_gray.cpp" "$P/gather.cpp" -lz -ldl > "$R/build_ab/$name.log" 2>&1 &
   pids+=($!)
 done
 rc=0

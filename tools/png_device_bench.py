@@ -2,7 +2,8 @@
 """Device PNG decode throughput (slg_png_decode_device): a rendered C2 capture's 44 PNG frames
 (PIL, as the tests write them), decoded in one launch as 1, 4 and 16 views' worth of frames.
 Prints one JSON line: ms per launch and per view, against the host decoder (slg_png_gray8_decode
-on 16 threads).  Run under rocprofv3 --kernel-trace --stats to split inflate from un-filter."""
+on 16 threads).  Run under rocprofv3 --kernel-trace --stats to split inflate from un-filter.
+--libs a.so,b.so: one subprocess per library (SLG_LIB), alternating, --rounds times."""
 from __future__ import annotations
 
 import ctypes
@@ -79,5 +80,24 @@ def main():
     print(json.dumps(out), flush=True)
 
 
+def ab():
+    import subprocess
+    libs = sys.argv[sys.argv.index("--libs") + 1].split(",")
+    rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 2
+    res = {lib: [] for lib in libs}
+    for r in range(rounds):
+        for lib in libs:
+            env = dict(os.environ, SLG_LIB=lib)
+            out = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
+                                 timeout=600)
+            if out.returncode != 0:
+                print(out.stderr[-3000:], file=sys.stderr)
+                raise SystemExit(f"{lib} failed")
+            d = json.loads(out.stdout.strip().splitlines()[-1])
+            res[lib].append(d)
+            print(f"[png-ab] round {r} {lib}: " + json.dumps({k: d[k] for k in d if k.startswith("views_")}), flush=True)
+    print(json.dumps({lib: min(x["views_16"]["ms_per_view"] for x in v) for lib, v in res.items()}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    ab() if "--libs" in sys.argv else main()
