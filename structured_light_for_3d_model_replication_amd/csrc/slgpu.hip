@@ -1548,8 +1548,23 @@ __device__ inline int bgr_slot(int m) { return m + (m >> SLG_BGR_PAD); }
 // goes to LDS word l (its index within the tile's kept points), and the workgroup writes the
 // tile's contiguous byte range [3 base, 3 (base + agg)) as 16-byte aligned stores, each lane
 // packing six staged words into four output dwords; the two ragged end chunks go byte by byte.
+#ifndef SLG_NT_STORES
+#define SLG_NT_STORES 0                    // phase D's XYZ / BGR stores non-temporal
+#endif
+#ifndef SLG_PRIO_A
+#define SLG_PRIO_A 0                       // s_setprio for phase A (decode: the frame stream) over B-D
+#endif
+template <typename T>
+__device__ inline void st_out(T* a, T v) {
+#if SLG_NT_STORES
+  __builtin_nontemporal_store(v, a);
+#else
+  *a = v;
+#endif
+}
+
 #ifndef SLG_BGR_STAGE
-#define SLG_BGR_STAGE 1
+#define SLG_BGR_STAGE 0                    // 329.3 vs 324.5 us per 16-view launch (profiles/r4j): off
 #endif
 constexpr int kStageWords = kTilePx + 8;          // + the 6-word read window past the last point
 
@@ -1696,6 +1711,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   }
   // ------------------------------------------------------------ A: decode + tile compaction
   int n_items;
+  if (SLG_PRIO_A) __builtin_amdgcn_s_setprio(SLG_PRIO_A);
   {
     uint32_t tex[6] = {0, 0, 0, 0, 0, 0};
     auto load_tex = [&]() {
@@ -1738,6 +1754,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     }
   }
   __syncthreads();
+  if (SLG_PRIO_A) __builtin_amdgcn_s_setprio(0);
 
   stamp(0);
   if (hn) {                                          // block-uniform; counted in phase C
@@ -1892,12 +1909,12 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
         const int64_t q = base + l;
         const uint32_t c = s_bgr[bgr_slot(tid + kB * i)];
         if (!(PROF && (p.dbg & 128))) {              // PROF ablation bit 7: no XYZ stores
-          gx[3 * q] = pts[s][i][0]; gx[3 * q + 1] = pts[s][i][1]; gx[3 * q + 2] = pts[s][i][2];
+          st_out(gx + 3 * q, pts[s][i][0]); st_out(gx + 3 * q + 1, pts[s][i][1]); st_out(gx + 3 * q + 2, pts[s][i][2]);
         }
         if (SLG_BGR_STAGE) {
           s_stage[s * kStageWords + l] = c;
         } else if (!(PROF && (p.dbg & 8))) {         // PROF ablation bit 3: no BGR stores
-          gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
+          st_out(gb + 3 * q, uint8_t(c)); st_out(gb + 3 * q + 1, uint8_t(c >> 8)); st_out(gb + 3 * q + 2, uint8_t(c >> 16));
         }
       }
     }

@@ -16,7 +16,7 @@
 #                    e.g. bench=c4=--config,c4   bench=2r=--gpus,2 (with SLG_BENCH_* exported)
 #   prof             kernel trace + FETCH/WRITE PMC passes (tools/gpu_profile.sh) -> <tag>/prof/
 #   sq               SQ counter passes (tools/pmc_main.sh)              -> <tag>/sq/
-#   ab=<libA>,<libB>[,rounds]   interleaved A/B of two library builds (tools/ab.py) -> ab.log
+#   ab=<libA>,<libB>[,...][,rounds]  interleaved A/B of library builds (tools/ab.py) -> ab.log
 #   py=<script>=<args>   python <script> <args> (commas -> spaces)      -> py_<n>.log
 #   mem              device memory as torch sees it                     -> mem.log
 set -o pipefail
@@ -56,8 +56,9 @@ for step in "$@"; do
     sq)
       bash "$R/tools/pmc_main.sh" "$TAG/sq" || { echo "[gpu.sh] SQ FAILED"; exit $n; } ;;
     ab)
-      IFS=, read -r la lb rounds <<< "$rest"
-      timeout -k 10 600 python tools/ab.py --libs "$la,$lb" --rounds "${rounds:-4}" > "$O/ab.log" 2>&1 \
+      libs=${rest%,[0-9]*}; rounds=${rest##*,}
+      [ "$libs" = "$rest" ] && rounds=4
+      timeout -k 10 900 python tools/ab.py --libs "$libs" --rounds "$rounds" > "$O/ab.log" 2>&1 \
         || { echo "[gpu.sh] AB FAILED"; tail -20 "$O/ab.log"; exit $n; }
       tail -3 "$O/ab.log" ;;
     py)

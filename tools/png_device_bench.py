@@ -82,7 +82,11 @@ def main():
 
 def ab():
     import subprocess
-    libs = sys.argv[sys.argv.index("--libs") + 1].split(",")
+    i = sys.argv.index("--libs") + 1                  # comma- or space-separated (tools/gpu.sh py=)
+    libs = []
+    while i < len(sys.argv) and not sys.argv[i].startswith("--"):
+        libs += [x for x in sys.argv[i].split(",") if x]
+        i += 1
     rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 2
     res = {lib: [] for lib in libs}
     for r in range(rounds):
