@@ -5,8 +5,9 @@
 // batch of frames:
 //
 // png_inflate_kernel -- one 64-lane wave per zlib stream.  The symbol decode is inherently
-//   serial, so it runs wave-uniform (bit buffer in SGPRs, Huffman tables and the 32 KB history
-//   ring in LDS, ~38 KB per wave: 4 streams per CU, 1024 in flight); LZ77 copies use all 64
+//   serial, so it runs wave-uniform (bit buffer in SGPRs, Huffman tables -- one of them giving
+//   up to 4 literals per lookup -- and the 32 KB history ring in LDS, 50 KB per wave: 3 streams
+//   per CU, 768 in flight); literal runs are written by 4 lanes, LZ77 copies by all 64
 //   lanes (a copy whose distance is under 64 repeats its period, so no lane reads a byte the
 //   copy itself has yet to write).  Inflated scanlines go to the frame's raw scratch.
 // png_unfilter_kernel -- one wave per frame undoes the five scanline filters (PNG §9) over
@@ -26,24 +27,44 @@ int slg_internal_fail(int code, const char* fmt, ...);
 
 namespace {
 
-constexpr int kRing = 40960;                // LDS output ring: the 32 KB deflate window + what is
-constexpr int kFlush = 4096;                //   not yet flushed to the frame's raw scratch (flushed
-                                            //   4 KB at a time by the whole wave; 46 KB of LDS per
-                                            //   wave: 3 streams per CU, 768 in flight)
+constexpr int kRing = 36864;                // LDS output ring: the 32 KB deflate window + what is
+constexpr int kFlush = 2048;                //   not yet flushed to the frame's raw scratch (flushed
+                                            //   2 KB at a time by the whole wave; < 2048 + 258
+                                            //   unflushed bytes).  50 KB of LDS per wave with the
+                                            //   tables: 3 streams per CU, 768 in flight
 constexpr int kFastBits = 10;               // primary Huffman table index bits
 constexpr int kAdlerMod = 65521;
 constexpr int kMaxRowBytes = 24576;         // device un-filter: rows up to 24 KB (6000 px RGBA: host)
 
-__constant__ uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
-                                      35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2,
-                                      3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t kDistBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193,
-                                       257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145,
-                                       8193, 12289, 16385, 24577};
-__constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6,
-                                       7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+// RFC 1951 §3.2.5 length / distance bases and extra bits, computed (SALU) rather than read from
+// tables: a table read is a vector-memory round trip on every match's serial chain.
+// Length code 257 + s: s < 8 -> 3 + s; s == 28 -> 258; else e = (s - 4) / 4 extra bits on
+// ((4 + s % 4) << e) + 3.  Distance code d: d < 4 -> d + 1; else e = d / 2 - 1 on
+// ((2 + d % 2) << e) + 1.
+__device__ inline uint32_t len_extra(uint32_t s) { return (s < 8u || s == 28u) ? 0u : (s - 4u) >> 2; }
+__device__ inline uint32_t len_base(uint32_t s) {
+  return s < 8u ? s + 3u : s == 28u ? 258u : ((4u + (s & 3u)) << len_extra(s)) + 3u;
+}
+__device__ inline uint32_t dist_extra(uint32_t d) { return d < 4u ? 0u : (d >> 1) - 1u; }
+__device__ inline uint32_t dist_base(uint32_t d) { return d < 4u ? d + 1u : ((2u + (d & 1u)) << dist_extra(d)) + 1u; }
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// PNG_PROF builds (tools/png_device_bench.py --prof): per-launch sums of event counts and
+// 100 MHz timer intervals over all streams, read back by slg_png_prof_read; PNG_ABL bits switch
+// parts off for timing (the output is then wrong): 1 literal LDS writes, 2 match copies,
+// 4 ring flushes.
+#ifndef PNG_PROF
+#define PNG_PROF 0
+#endif
+#ifndef PNG_ABL
+#define PNG_ABL 0
+#endif
+enum { kPfTotal, kPfBuild, kPfHeader, kPfCopy, kPfFlush, kPfLit, kPfMatch, kPfMatchBytes, kPfBlocks,
+       kPfRuns, kPfSymbols, kPfN = 16 };
+#if PNG_PROF
+__device__ unsigned long long g_png_prof[kPfN];
+#endif
+__device__ inline uint64_t pf_now() { return PNG_PROF ? __builtin_amdgcn_s_memrealtime() : 0; }
 
 // Canonical Huffman code in LDS: a 2^kFastBits table for codes up to kFastBits bits (entry =
 // symbol | length << 9, 0 = longer code or none) and the counts + sorted symbols the slow
@@ -149,40 +170,38 @@ __device__ inline int decode(Bits& b, const Huff& h) {
   return int(r & 0xffffu);
 }
 
-// The primary table of a built code held in VGPRs (PNG_VTAB): entry pair d (entries 2d, 2d + 1)
-// in lane d % 64 of word d / 64.  A lookup is one indexed v_readlane into an SGPR, a few cycles,
-// where the LDS table costs an LDS round trip (~100 cycles) on the serial chain of every symbol.
-#ifndef PNG_VTAB
-#define PNG_VTAB 1
+// Literal runs: lit4[i] holds the literals that the 10 stream bits i decode to in a row, as long
+// as each code fits the bits still known (up to 4: bytes in bits 0-31, count in 32-35, bits used
+// in 36-39); a count of 0 (the first code is a length / end-of-block symbol, or longer than
+// 10 bits) falls back to decode().  PNG scanline residuals code in ~4 bits a byte, so one LDS
+// lookup on the serial chain yields ~2.5 literals instead of one.
+#ifndef PNG_LIT11
+#define PNG_LIT11 1                          // 11-bit index, 4-byte entries, <= 3 literals: 14.07 vs 16.28 ms/view (10-bit, 8-byte, <= 4; profiles/r4n)
 #endif
-typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
-static_assert((1 << kFastBits) / 128 == 8, "eight table words per lane");
-struct VTab {
-  u32x8 w;
-};
+#if PNG_LIT11
+constexpr int kLitBits = 11, kLitMax = 3;
+typedef uint32_t LitEntry;                   // bytes 0-23, count in 24-25, bits used in 26-29
+constexpr int kLitCountShift = 24;
+#else
+constexpr int kLitBits = kFastBits, kLitMax = 4;
+typedef uint64_t LitEntry;                   // bytes 0-31, count in 32-35, bits used in 36-39
+constexpr int kLitCountShift = 32;
+#endif
 
-__device__ inline void vtab_load(VTab& t, const Huff& h) {
-  const uint32_t* f = reinterpret_cast<const uint32_t*>(h.fast);
-#pragma unroll
-  for (int r = 0; r < 8; ++r) t.w[r] = f[r * 64 + int(threadIdx.x)];
-}
-
-__device__ inline int decode(Bits& b, const VTab& t, const Huff& h) {
-  refill(b);
-  const uint32_t idx = uint32_t(b.buf) & ((1u << kFastBits) - 1u);
-  const uint32_t d = idx >> 1;
-  // lane d % 64 of all eight words (independent readlanes, pipelined) into SGPRs, then word d / 64
-  u32x8 sw;
-#pragma unroll
-  for (int r = 0; r < 8; ++r) sw[r] = __builtin_amdgcn_readlane(t.w[r], int(d & 63u));
-  const uint32_t pair = sw[d >> 6];
-  const uint32_t e = (pair >> ((idx & 1u) * 16u)) & 0xffffu;
-  const uint32_t r = (e >> 9) ? ((e & 511u) | ((e >> 9) << 16)) : uni(decode_slow(b.buf, h));
-  if (r == ~0u) return -1;
-  const int len = int(r >> 16);
-  b.buf >>= len;
-  b.cnt -= len;
-  return int(r & 0xffffu);
+__device__ inline void build_lit4(LitEntry* lit4, const Huff& h) {
+  for (int i = int(threadIdx.x); i < (1 << kLitBits); i += 64) {
+    uint32_t idx = uint32_t(i), used = 0, n = 0, lits = 0;
+    while (n < uint32_t(kLitMax)) {
+      const uint32_t e = h.fast[idx & ((1u << kFastBits) - 1u)];
+      const uint32_t l = e >> 9, sym = e & 511u;
+      if (l == 0 || used + l > uint32_t(kLitBits) || sym >= 256u) break;
+      lits |= sym << (8 * n);
+      ++n;
+      used += l;
+      idx >>= l;
+    }
+    lit4[i] = LitEntry(lits) | (LitEntry(n | (used << 4)) << kLitCountShift);
+  }
 }
 
 // Build `h` from code lengths lens[0..n) (LDS); all 64 lanes call it.  False for an
@@ -232,12 +251,13 @@ __device__ __attribute__((noinline)) bool build(Huff& h, const uint8_t* lens, in
 
 struct InflateLds {
   alignas(16) uint8_t ring[kRing];
+  LitEntry lit4[1 << kLitBits];
   Huff lit, dist;
   uint8_t lens[320];                      // litlen code lengths at [0, 288), distance at [288, 320)
   uint32_t work[48];
 };
 
-// Ring bytes [flushed, flushed + n) -> raw[flushed ...], by all lanes: whole 4 KB blocks as
+// Ring bytes [flushed, flushed + n) -> raw[flushed ...], by all lanes: whole kFlush blocks as
 // 16-byte moves, the final ragged part byte by byte.
 __device__ inline void flush_ring(const uint8_t* ring, __amdgpu_buffer_rsrc_t out, int64_t flushed, int n) {
   const int lane = threadIdx.x;
@@ -266,28 +286,38 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
   __shared__ InflateLds L;
   const int lane = threadIdx.x;
   const slg_png_frame f = frames[blockIdx.x];
-  const int64_t row = 1 + int64_t(f.width) * f.channels;
-  const int64_t n_out = int64_t(f.height) * row;
+  // (the descriptor is a vector load: its sizes re-read as wave-uniform SGPR values)
+  const int64_t row = 1 + int64_t(int32_t(uni(uint32_t(f.width)))) * int32_t(uni(uint32_t(f.channels)));
+  const int64_t n_out64 = int64_t(int32_t(uni(uint32_t(f.height)))) * row;
+  const int32_t n_out = n_out64 < INT32_MAX ? int32_t(n_out64) : 0;    // (32-bit positions: SALU compares)
   Bits b;
   bits_init(b, f.z, f.zlen);
   const __amdgpu_buffer_rsrc_t out = uni_rsrc(f.raw, uint32_t(n_out));
   int err = 0;
-  int64_t pos = 0, flushed = 0;
+  int32_t pos = 0, flushed = 0;
+  if (n_out64 >= INT32_MAX) err = SLG_PNG_E_UNSUPPORTED;
   int ridx = 0;                                            // pos % kRing
+  uint64_t pf[kPfN] = {};
+  const uint64_t pf_t0 = pf_now();
+  auto flush4k = [&]() {
+    const uint64_t t = pf_now();
+    if (!(PNG_ABL & 4)) flush_ring(L.ring, out, flushed, kFlush);
+    flushed += kFlush;
+    if (PNG_PROF) pf[kPfFlush] += pf_now() - t;
+  };
   auto put = [&](uint8_t v) {                              // one literal byte (lane 0 writes)
-    if (lane == 0) L.ring[ridx] = v;
+    if (lane == 0 && !(PNG_ABL & 1)) L.ring[ridx] = v;
     ++pos;
     if (++ridx == kRing) ridx = 0;
-    if (pos - flushed == kFlush) {
-      flush_ring(L.ring, out, flushed, kFlush);
-      flushed += kFlush;
-    }
+    if (pos - flushed >= kFlush) flush4k();
   };
   // zlib header: deflate, 32 KB window at most, no preset dictionary, check bits
   const uint32_t cmf = getbits(b, 8), flg = getbits(b, 8);
   if ((cmf & 15u) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 != 0 || (flg & 0x20u)) err = SLG_PNG_E_STREAM;
   bool last = false;
   while (!err && !last) {
+    if (PNG_PROF) ++pf[kPfBlocks];
+    const uint64_t pf_th = pf_now();
     last = getbits(b, 1) != 0;
     const uint32_t type = getbits(b, 2);
     if (type == 0) {                                         // stored block
@@ -295,7 +325,7 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
       b.buf >>= drop;
       b.cnt -= drop;
       const uint32_t len = getbits(b, 16), nlen = getbits(b, 16);
-      if ((len ^ 0xffffu) != nlen || pos + len > n_out) { err = SLG_PNG_E_STREAM; break; }
+      if ((len ^ 0xffffu) != nlen || pos + int32_t(len) > n_out) { err = SLG_PNG_E_STREAM; break; }
       for (uint32_t k = 0; k < len; ++k) {
         put(uint8_t(getbits(b, 8)));
       }
@@ -352,40 +382,57 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
       __syncthreads();
       if (L.lens[256] == 0) { err = SLG_PNG_E_STREAM; break; }
     }
+    const uint64_t pf_tb = pf_now();
     if (!uni(build(L.lit, L.lens, hlit, L.work)) || !uni(build(L.dist, L.lens + 288, hdist, L.work))) {
       err = SLG_PNG_E_STREAM;
       break;
     }
-#if PNG_VTAB
-    VTab vlit, vdist;
-    vtab_load(vlit, L.lit);
-    vtab_load(vdist, L.dist);
-#define PNG_LIT vlit, L.lit
-#define PNG_DIST vdist, L.dist
-#else
-#define PNG_LIT L.lit
-#define PNG_DIST L.dist
-#endif
+    if (PNG_PROF) { pf[kPfBuild] += pf_now() - pf_tb; pf[kPfHeader] += pf_tb - pf_th; }
+    build_lit4(L.lit4, L.lit);
+    __syncthreads();
     for (;;) {                                               // the block's symbols
-      int s = decode(b, PNG_LIT);
+      refill(b);
+      const LitEntry e4 = L.lit4[uint32_t(b.buf) & ((1u << kLitBits) - 1u)];
+      const uint32_t cu = uni(uint32_t(e4 >> kLitCountShift));
+      const uint32_t n4 = cu & 15u;
+      if (n4) {                                              // a run of 1-4 literals
+        const uint32_t used = (cu >> 4) & 15u;
+        b.buf >>= used;
+        b.cnt -= int(used);
+        if (pos + int32_t(n4) > n_out) { err = SLG_PNG_E_SIZE; break; }
+        if (lane < int(n4) && !(PNG_ABL & 1)) {              // lane k writes literal k
+          int r = ridx + lane;
+          if (r >= kRing) r -= kRing;
+          L.ring[r] = uint8_t(uint32_t(e4) >> (8 * lane));
+        }
+        pos += int32_t(n4);
+        ridx += int(n4);
+        if (ridx >= kRing) ridx -= kRing;
+        if (pos - flushed >= kFlush) flush4k();
+        if (PNG_PROF) { pf[kPfLit] += n4; ++pf[kPfRuns]; }
+        continue;
+      }
+      int s = decode(b, L.lit);
       if (s < 0) { err = SLG_PNG_E_STREAM; break; }
       if (s < 256) {
         if (pos >= n_out) { err = SLG_PNG_E_SIZE; break; }
         put(uint8_t(s));
+        if (PNG_PROF) ++pf[kPfLit];
         continue;
       }
       if (s == 256) break;
       s -= 257;
       if (s >= 29) { err = SLG_PNG_E_STREAM; break; }
-      const int len = int(kLenBase[s]) + int(getbits(b, kLenExtra[s]));
-      const int ds = decode(b, PNG_DIST);
+      const int len = int(len_base(uint32_t(s))) + int(getbits(b, int(len_extra(uint32_t(s)))));
+      const int ds = decode(b, L.dist);
       if (ds < 0 || ds >= 30) { err = SLG_PNG_E_STREAM; break; }
-      const int dist = int(kDistBase[ds]) + int(getbits(b, kDistExtra[ds]));
+      const int dist = int(dist_base(uint32_t(ds))) + int(getbits(b, int(dist_extra(uint32_t(ds)))));
       if (dist > pos) { err = SLG_PNG_E_STREAM; break; }
       if (pos + len > n_out) { err = SLG_PNG_E_SIZE; break; }
       __builtin_amdgcn_wave_barrier();
+      const uint64_t pf_tc = pf_now();
       const int sbase = ridx >= dist ? ridx - dist : ridx - dist + kRing;
-      for (int c = 0; c < len; c += 64) {                    // all lanes; 64 bytes per step
+      for (int c = 0; c < ((PNG_ABL & 2) ? 0 : len); c += 64) {   // all lanes; 64 bytes per step
         const int i = c + lane;
         if (i < len) {
           int si = sbase + (dist >= 64 ? i : i % dist), di = ridx + i;
@@ -395,13 +442,11 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
         }
         __builtin_amdgcn_wave_barrier();
       }
+      if (PNG_PROF) { pf[kPfCopy] += pf_now() - pf_tc; ++pf[kPfMatch]; pf[kPfMatchBytes] += len; }
       pos += len;
       ridx += len;
       if (ridx >= kRing) ridx -= kRing;
-      if (pos - flushed >= kFlush) {                         // (len <= 258: at most one block)
-        flush_ring(L.ring, out, flushed, kFlush);
-        flushed += kFlush;
-      }
+      if (pos - flushed >= kFlush) flush4k();                // (len <= 258: at most one block)
     }
   }
   if (!err && pos != n_out) err = SLG_PNG_E_SIZE;
@@ -416,6 +461,12 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
     status[2 * blockIdx.x] = err;
     status[2 * blockIdx.x + 1] = int32_t(adler);
   }
+#if PNG_PROF
+  pf[kPfTotal] = pf_now() - pf_t0;
+  pf[kPfSymbols] = pf[kPfLit] + pf[kPfMatch];                // (literals, not lookups)
+  if (lane == 0)
+    for (int k = 0; k < kPfN; ++k) atomicAdd(&g_png_prof[k], (unsigned long long)pf[k]);
+#endif
 }
 
 // Wavefront un-filter + Adler-32 check of one frame (status from png_inflate_kernel).
@@ -530,6 +581,18 @@ int64_t slg_png_raw_bytes(int32_t width, int32_t height, int32_t channels) {
   if (width <= 0 || height <= 0 || channels < 1 || channels > 4) return -SLG_ERR_INVALID;
   return (int64_t(height) * (1 + int64_t(width) * channels) + 15) / 16 * 16;
 }
+
+// PNG_PROF builds only (not in include/slgpu.h): copy the counters out, optionally zero them.
+#if PNG_PROF
+int32_t slg_png_prof_read(uint64_t* out, int32_t reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_png_prof), sizeof(uint64_t) * kPfN) != hipSuccess) return SLG_ERR_HIP;
+  if (reset) {
+    static const uint64_t zero[kPfN] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_png_prof), zero, sizeof(zero)) != hipSuccess) return SLG_ERR_HIP;
+  }
+  return SLG_OK;
+}
+#endif
 
 int32_t slg_png_decode_device(const slg_png_frame* frames, int32_t n, int32_t* status, void* stream) {
   if (n < 0 || (n > 0 && (!frames || !status))) return slg_internal_fail(SLG_ERR_INVALID, "slg_png_decode_device: bad argument");

@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--views", type=int, default=16)
-    ap.add_argument("--groups", type=int, nargs="+", default=[1, 4])
+    ap.add_argument("--groups", type=int, nargs="+", default=[1, 4, 16])
     args = ap.parse_args()
 
     from structured_light_for_3d_model_replication_amd import calibration, synth

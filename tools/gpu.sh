@@ -18,6 +18,7 @@
 #   sq               SQ counter passes (tools/pmc_main.sh)              -> <tag>/sq/
 #   ab=<libA>,<libB>[,...][,rounds]  interleaved A/B of library builds (tools/ab.py) -> ab.log
 #   py=<script>=<args>   python <script> <args> (commas -> spaces)      -> py_<n>.log
+#   kt=<script>=<args>   the same under rocprofv3 --kernel-trace --stats  -> kt_<n>/ (+ kt_<n>.log)
 #   mem              device memory as torch sees it                     -> mem.log
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -67,6 +68,13 @@ for step in "$@"; do
       timeout -k 10 600 python "$script" ${args//,/ } > "$O/py_$n.log" 2>&1 \
         || { echo "[gpu.sh] PY $script FAILED"; tail -30 "$O/py_$n.log"; exit $n; }
       tail -5 "$O/py_$n.log" ;;
+    kt)
+      script=${rest%%=*}; args=${rest#*=}
+      [ "$args" = "$rest" ] && args=""
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/kt_$n" -o kt \
+        --output-format csv -- python "$R/$script" ${args//,/ } > "$O/kt_$n.log" 2>&1) \
+        || { echo "[gpu.sh] KT $script FAILED"; tail -30 "$O/kt_$n.log"; exit $n; }
+      head -12 "$O/kt_$n/kt_kernel_stats.csv" 2>/dev/null || find "$O/kt_$n" -name "*kernel_stats.csv" -exec head -12 {} \; ;;
     mem)
       timeout -k 10 120 python -c "import torch; f,t=torch.cuda.mem_get_info(0); print('free',f,'total',t,torch.cuda.get_device_name(0))" > "$O/mem.log" 2>&1 \
         || { echo "[gpu.sh] MEM FAILED"; cat "$O/mem.log"; exit $n; }

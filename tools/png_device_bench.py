@@ -60,6 +60,22 @@ def main():
                                                 ctypes.c_void_p(s.cuda_stream)))
                 torch.cuda.synchronize()
                 times.append(time.perf_counter() - t)
+            if hasattr(L, "slg_png_prof_read"):          # PNG_PROF build: counters of the last launch
+                pfv = (ctypes.c_uint64 * 16)()
+                L.slg_png_prof_read(pfv, 1)
+                torch.cuda.synchronize()
+                N.check(L.slg_png_decode_device(ctypes.c_void_p(d.data_ptr()), n, ctypes.c_void_p(status.data_ptr()),
+                                                ctypes.c_void_p(s.cuda_stream)))
+                torch.cuda.synchronize()
+                L.slg_png_prof_read(pfv, 1)
+                names = ["total", "build", "header", "copy", "flush", "lit", "match", "match_bytes", "blocks",
+                         "slow", "symbols"]
+                per = {k: pfv[i] / n for i, k in enumerate(names)}
+                for k in ("total", "build", "header", "copy", "flush"):
+                    per[k + "_ms"] = round(per.pop(k) * 1e-5, 3)    # 100 MHz ticks per stream -> ms
+                per = {k: (round(v, 1) if not k.endswith("_ms") else v) for k, v in per.items()}
+                per["ns_per_symbol_total"] = round(per["total_ms"] * 1e6 / max(per["symbols"], 1), 1)
+                out[f"prof_views_{views}"] = per
             ok = bool((status.view(-1, 2)[:, 0] == 0).all().item())
             same = bool(torch.equal(frames[0].cpu(), torch.from_numpy(v.frames[0].reshape(-1))))
             out[f"views_{views}"] = {"frames": n, "ms_per_launch": round(1e3 * min(times), 2),
@@ -99,7 +115,7 @@ def ab():
                 raise SystemExit(f"{lib} failed")
             d = json.loads(out.stdout.strip().splitlines()[-1])
             res[lib].append(d)
-            print(f"[png-ab] round {r} {lib}: " + json.dumps({k: d[k] for k in d if k.startswith("views_")}), flush=True)
+            print(f"[png-ab] round {r} {lib}: " + json.dumps({k: d[k] for k in d if k.startswith(("views_16", "prof_views_16"))}), flush=True)
     print(json.dumps({lib: min(x["views_16"]["ms_per_view"] for x in v) for lib, v in res.items()}), flush=True)
 
 
