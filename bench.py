@@ -218,11 +218,13 @@ def cpu_baseline_only(args, rank: int, world: int, cpu) -> None:
               file=getattr(args, "result_out", None) or RESULT_OUT, flush=True)
 
 
-def load_traffic_per_view():
-    """The committed rocprofv3 PMC summary of the fused kernel on the C2 bench shape
-    (profiles/pmc_main_kernel.json: HBM bytes per view, reads from the gfx950 request-size
-    counters as calibrated by tools/fetch_probe.hip, writes from WRITE_SIZE), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_main_kernel.json")
+def load_traffic_per_view(config: str = "c2"):
+    """The committed rocprofv3 PMC summary of the fused kernel on this config's bench shape
+    (profiles/pmc_main_kernel.json for C2, pmc_main_kernel_<config>.json otherwise: HBM bytes
+    per view, reads from the gfx950 request-size counters as calibrated by
+    tools/fetch_probe.hip, writes from WRITE_SIZE), or None."""
+    name = "pmc_main_kernel.json" if config == "c2" else f"pmc_main_kernel_{config}.json"
+    p = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(p):
         return None
     try:
@@ -590,7 +592,8 @@ def main():
         kern_avg_s = kern_sum / launches / 1e3
         achieved = dense_sum / launches / kern_avg_s / 1e9          # SURVEY 8(d)'s algorithmic bytes
         mf_achieved = bytes_sum / launches / kern_avg_s / 1e9       # the mask-first decode's own bytes
-        pmc = load_traffic_per_view() if args.config == "c2" else None
+        pmc = load_traffic_per_view(args.config) if args.config in ("c2", "c4", "c5") else None
+        pmc_name = "pmc_main_kernel.json" if args.config == "c2" else f"pmc_main_kernel_{args.config}.json"
         traffic_view = pmc["hbm_bytes_per_view"] if pmc else None
         n_pts_mean = float(np.mean(pts))
         model = {k: round(float(np.mean([m[k] for m in models]))) for k in models[0]}
@@ -608,9 +611,9 @@ def main():
             traffic_model["measured_over_model"] = round(traffic_view / model["total_with_writes"], 4)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                # committed PMC bytes (profiles/pmc_main_kernel.json) are per C2 view
+                # committed PMC bytes (profiles/pmc_main_kernel*.json) are per view of this config
                 "traffic": round(traffic_view * B) if traffic_view else None,
-                "traffic_source": ("profiles/pmc_main_kernel.json (rocprofv3 per launch: reads 128 x RDREQ_128B + "
+                "traffic_source": (f"profiles/{pmc_name} (rocprofv3 per launch: reads 128 x RDREQ_128B + "
                                    "64 x RDREQ_64B + 32 x RDREQ_32B, = FETCH_SIZE x 2 since all reads are 128-B "
                                    "requests, calibrated on known byte counts in profiles/r4c; writes WRITE_SIZE)")
                 if traffic_view else None,

@@ -15,6 +15,7 @@
 #   bench=<name>=<args>   python bench.py <args> (commas -> spaces)     -> bench_<name>.json / .err
 #                    e.g. bench=c4=--config,c4   bench=2r=--gpus,2 (with SLG_BENCH_* exported)
 #   prof             kernel trace + FETCH/WRITE PMC passes (tools/gpu_profile.sh) -> <tag>/prof/
+#   prof=<name>=<args>   the same for bench.py <args> (commas -> spaces)  -> <tag>/prof_<name>/
 #   sq               SQ counter passes (tools/pmc_main.sh)              -> <tag>/sq/
 #   ab=<libA>,<libB>[,...][,rounds]  interleaved A/B of library builds (tools/ab.py) -> ab.log
 #   py=<script>=<args>   python <script> <args> (commas -> spaces)      -> py_<n>.log
@@ -53,7 +54,12 @@ for step in "$@"; do
         || { echo "[gpu.sh] BENCH $name FAILED"; tail -20 "$O/bench_$name.err"; exit $n; }
       cat "$O/bench_$name.json" ;;
     prof)
-      bash "$R/tools/gpu_profile.sh" "$TAG/prof" || { echo "[gpu.sh] PROF FAILED"; exit $n; } ;;
+      if [ -n "$rest" ]; then
+        pname=${rest%%=*}; pargs=${rest#*=}
+        PMC_TIMEOUT=300 BENCH_ARGS="${pargs//,/ }" bash "$R/tools/gpu_profile.sh" "$TAG/prof_$pname" || { echo "[gpu.sh] PROF $pname FAILED"; exit $n; }
+      else
+        bash "$R/tools/gpu_profile.sh" "$TAG/prof" || { echo "[gpu.sh] PROF FAILED"; exit $n; }
+      fi ;;
     sq)
       bash "$R/tools/pmc_main.sh" "$TAG/sq" || { echo "[gpu.sh] SQ FAILED"; exit $n; } ;;
     ab)

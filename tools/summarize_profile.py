@@ -33,16 +33,26 @@ def rows_of(path, kernel):
         return [r for r in csv.DictReader(f) if kernel in r["Kernel_Name"]]
 
 
+TILES_PER_VIEW = {"c2": 507, "c4": 5860, "c5": 2025}     # ceil(H*W / 4096): 1920x1080, 6000x4000, 3840x2160
+
+
+def pmc_file(config: str) -> str:
+    return "pmc_main_kernel.json" if config == "c2" else f"pmc_main_kernel_{config}.json"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
     ap.add_argument("--kernel", default="main3_kernel")
-    ap.add_argument("--tiles-per-view", type=int, default=507, help="ceil(1920*1080 / 4096)")
+    ap.add_argument("--config", default="c2", choices=tuple(TILES_PER_VIEW),
+                    help="bench config profiled: sets --tiles-per-view and which profiles/pmc_main_kernel*.json "
+                         "is refreshed (c2: pmc_main_kernel.json, else pmc_main_kernel_<config>.json)")
+    ap.add_argument("--tiles-per-view", type=int, default=0, help="default: ceil(H*W / 4096) of --config")
     ap.add_argument("--timed-last", type=int, default=0,
                     help="also report the mean over the last N launches of the most frequent grid (the "
                          "bench's timed steps: the trace run's --steps; settle/warmup launches excluded)")
     ap.add_argument("--no-refresh", action="store_true",
-                    help="leave profiles/pmc_main_kernel.json (bench.py's C2 traffic) untouched")
+                    help="leave profiles/pmc_main_kernel*.json (bench.py's traffic figures) untouched")
     a = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", a.tag)
     dst = os.path.join(ROOT, "profiles", a.tag)
@@ -51,7 +61,7 @@ def main():
                  ("bench_trace.json", "bench_trace.json")):
         if os.path.exists(os.path.join(src, s)):
             shutil.copy(os.path.join(src, s), os.path.join(dst, d))
-    grid_threads_per_view = LANES * a.tiles_per_view
+    grid_threads_per_view = LANES * (a.tiles_per_view or TILES_PER_VIEW[a.config])
 
     # kernel trace: duration per launch grouped by grid size
     by_grid = collections.defaultdict(list)
@@ -113,8 +123,8 @@ def main():
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     if per and not a.no_refresh:
-        with open(os.path.join(ROOT, "profiles", "pmc_main_kernel.json"), "w") as f:
-            json.dump({"tag": a.tag, "kernel": a.kernel, "hbm_bytes_per_view": out["hbm_bytes_per_view"],
+        with open(os.path.join(ROOT, "profiles", pmc_file(a.config)), "w") as f:
+            json.dump({"tag": a.tag, "config": a.config, "kernel": a.kernel, "hbm_bytes_per_view": out["hbm_bytes_per_view"],
                        "fetch_bytes_per_view": round(per["FETCH_SIZE"]) if "FETCH_SIZE" in per else None,
                        "write_bytes_per_view": out.get("write_size_bytes_per_view"),
                        "formula": out["units"]}, f, indent=1)
