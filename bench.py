@@ -281,7 +281,7 @@ def mask_first_segments(frames, cfg, H, W, dev, block: int = 64) -> int:
     return segments_holding(mask, frames.stride, range(2, n), block)
 
 
-def read_model(frames, cfg, H, W, dev, carried: bool = True) -> dict:
+def read_model(frames, cfg, H, W, dev, carried: bool = True, texture: bool = True) -> dict:
     """The HBM bytes one view's fused launch reads, piece by piece, at the 128-byte request size
     rocprofv3 shows for every main3 read (profiles/r4c/pmc_calibration.json: RDREQ_128B ~ all
     requests; tools/fetch_probe.hip's mask-gated 8 B/lane reads fetch exactly the 128-B lines
@@ -293,7 +293,7 @@ def read_model(frames, cfg, H, W, dev, carried: bool = True) -> dict:
     dense = 2 * ((n_px + 127) // 128) * 128
     out = {"white_black": dense,
            "pattern_lines128": 128 * mask_first_segments(frames, cfg, H, W, dev, 128),
-           "texture_lines128": 128 * texture_lines_holding(mask, 128),
+           "texture_lines128": 128 * texture_lines_holding(mask, 128) if texture else 0,
            "carried_white_black": dense if carried else 0}
     out["total"] = sum(out.values())
     return out
@@ -360,6 +360,9 @@ def main():
     ap.add_argument("--copies", type=int, default=None, help="device copies of each view in the pool")
     ap.add_argument("--batch", type=int, default=None, help="views per fused launch (<= 16)")
     ap.add_argument("--xyz", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--gray-texture", action="store_true",
+                    help="gray captures (the reference scanner's 8-bit gray PNGs): the texture is frame 0 "
+                         "replicated, run in GRAY texture mode (no texture reads); default: a colour texture")
     ap.add_argument("--objects", type=int, default=8, help="c5job: objects in the job")
     ap.add_argument("--views-per-object", type=int, default=72, help="c5job: turntable views per object")
     ap.add_argument("--distinct", type=int, default=1, help="c5job: rendered captures per object")
@@ -439,7 +442,11 @@ def main():
     # Device pool: every rendered view uploaded `copies` times (distinct HBM buffers), so a batch
     # never shares frames with the batch before or after next -- e.g. the histograms a fused
     # launch computes for batch k+2 are cold HBM reads, as in a real turntable stream.
-    dframes = [E.DeviceFrames(list(v.frames), v.texture, device=dev) for _ in range(args.copies) for v in views]
+    if args.gray_texture:                             # cv2.imread(files[0]) of a gray PNG capture
+        for v in views:
+            v.texture = np.repeat(np.asarray(v.frames[0])[..., None], 3, axis=-1)
+    dframes = [E.DeviceFrames(list(v.frames), E.GRAY if args.gray_texture else v.texture, device=dev)
+               for _ in range(args.copies) for v in views]
     P = len(dframes)
     dcal = E.DeviceCalib(cal, H, W, device=dev)
     B = max(1, min(args.batch, E.MAX_VIEWS_PER_LAUNCH, P))
@@ -467,7 +474,8 @@ def main():
         pts += [int(clouds[0][k].count.item()) for k in range(B)]
     pts = pts[:P]
     seg_frames = [mask_first_segments(dframes[v], cfg, H, W, dev) for v in range(P)]
-    models = [read_model(dframes[v], cfg, H, W, dev, carried=args.pipeline in ("fused", "fused2")) for v in range(P)]
+    models = [read_model(dframes[v], cfg, H, W, dev, carried=args.pipeline in ("fused", "fused2"),
+                         texture=not args.gray_texture) for v in range(P)]
 
     K, Wm = args.steps, args.warmup
     # the whole run as ONE batch stream: warmup + timed + 2 look-ahead batches whose thresholds
@@ -483,6 +491,8 @@ def main():
     torch.cuda.synchronize()
     frame_b = (2 + 2 * (NC + NR)) * H * W
     out_b = 30 if f64 else 18            # 3 B texture read + 12|24 B XYZ + 3 B BGR per point
+    if args.gray_texture:
+        out_b -= 3                       # GRAY mode: the colour comes from the white frame, no texture read
 
     def pool_views(b):
         return [(b * B + k) % P for k in range(B)]
@@ -618,7 +628,8 @@ def main():
                                    "requests, calibrated on known byte counts in profiles/r4c; writes WRITE_SIZE)")
                 if traffic_view else None,
                 "traffic_model": traffic_model,
-                "kernel": (f"main3_kernel<1,{int(f64)},1,1,false,PLAN=0x{(NC << 4) | NR:X}> (fused decode+triangulate+"
+                "kernel": (f"main3_kernel<1,{int(f64)},1,1,false,PLAN=0x{(0x100 if args.gray_texture else 0) | (NC << 4) | NR:X}> "
+                           f"(fused decode+triangulate+"
                            f"compaction, decode-plan instance, {B} views per launch)"
                            if (NC, NR) in ((11, 10), (11, 11), (12, 12)) else
                            f"main3_kernel<1,{int(f64)},1,1> (fused decode+triangulate+compaction, {B} views per launch)"),
@@ -627,8 +638,10 @@ def main():
                                 else "HIP events around the timed region (both launch streams joined) / steps: "
                                      "the step period, gaps included"),
                 "alg_bytes_per_launch": round(dense_sum / launches),
-                "alg_bytes": "SURVEY 8(d): (2 + 2(nc+nr)) B per pixel (every frame once) + 18 B per point "
-                             "(3 B texture read, 12 B XYZ, 3 B BGR written)",
+                "alg_bytes": ("SURVEY 8(d): (2 + 2(nc+nr)) B per pixel (every frame once) + 18 B per point "
+                              "(3 B texture read, 12 B XYZ, 3 B BGR written)" if not args.gray_texture else
+                              "SURVEY 8(d) without the texture read: (2 + 2(nc+nr)) B per pixel + 15 B per point "
+                              "(12 B XYZ, 3 B BGR written; a gray capture's colour is its white frame)"),
                 # the kernel reads a pattern frame only where a lane holds a valid pixel (SLG_MASK_FIRST),
                 # so it moves fewer bytes than SURVEY's figure: the same time over the bytes it needs
                 "mask_first": {"alg_bytes_per_launch": round(bytes_sum / launches),
@@ -648,7 +661,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"{wl['text']}, Otsu, row_mode 1 tol 2.0, XYZ {args.xyz} + BGR out",
+            "config": {"workload": f"{wl['text']}, Otsu, row_mode 1 tol 2.0, XYZ {args.xyz} + BGR out"
+                                   + (", gray capture (texture = frame 0, GRAY mode)" if args.gray_texture else ""),
                        "step": f"one batch of {B} views: one fused launch + its thresholds (steady-state pipeline)",
                        "us_per_view": round(dt_max / (K * B) * 1e6, 3),
                        "cold_start_ms": round(cold_ms, 3),

@@ -86,7 +86,9 @@ typedef struct slg_capture {
   int32_t height;
   int32_t width;
   int32_t reserved;
-  const uint8_t *texture;  /* device, [height*width][3] BGR (cv2.imread(files[0])) */
+  const uint8_t *texture;  /* device, [height*width][3] BGR (cv2.imread(files[0])), or NULL for a
+                              gray capture: BGR = frame 0 replicated, what cv2.imread(files[0])
+                              returns for an 8-bit gray PNG (no texture bytes are then read) */
 } slg_capture;
 
 typedef struct slg_decode_params {

@@ -836,7 +836,7 @@ __device__ inline uint2 ld_frame8(const MainParams& p, int frame, int64_t lp) {
 // memory system then fetches only the 64-byte segments a valid pixel lies in.  `pre()` runs once
 // the lane is known to hold a valid pixel, before its pattern loads (the texture loads).
 struct NoPre {
-  __device__ void operator()() const {}
+  __device__ void operator()(uint2) const {}
 };
 
 // PLAN: (col_pairs << 4) | row_pairs as compile-time constants (main3's specialised instances for
@@ -864,10 +864,10 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
         row[k] = 0;
       }
       if (valid == 0u) return;
-      pre();
+      pre(w);                                     // (white bytes: a gray capture's texture)
     }
     PlaneAcc qc = {{0, 0}, {0, 0}}, qr = {{0, 0}, {0, 0}};
-    const int np_c = PLAN ? (PLAN >> 4) : p.col_pairs;
+    const int np_c = PLAN ? ((PLAN >> 4) & 15) : p.col_pairs;
     const int np_r = ROW_MODE == 0 ? 0 : (PLAN ? (PLAN & 15) : p.row_pairs);
     // compile-time trip count (kMaxBits pairs max), fully unrolled: only forward, wave-uniform
     // branches remain, so the loads of a batch stay in flight together (no vmcnt(0) per load)
@@ -1649,6 +1649,8 @@ __device__ inline void tri_rounds(const MainParams& p, int i, int n_items, const
 
 // PROF: the profiling instance (SLG_DBG set): honours the ablation bits of MainParams::dbg and
 // writes per-workgroup phase records; the production instances carry none of that code.
+constexpr int kPlanGray = 0x100;           // PLAN bit: every view of the launch is a gray capture
+
 template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS, bool PROF, int PLAN = 0>
 __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) void main3_kernel(Main3Params P) {
   using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
@@ -1721,8 +1723,17 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   if (SLG_PRIO_A) __builtin_amdgcn_s_setprio(SLG_PRIO_A);
   {
     uint32_t tex[6] = {0, 0, 0, 0, 0, 0};
-    auto load_tex = [&]() {
-      if (!tail) {
+    // texture NULL: a gray capture, whose cv2.imread(files[0]) is frame 0 replicated -- the white
+    // bytes decode_lane has already read give the colour, no texture bytes are read at all.
+    // Plan instances fix it at compile time (kPlanGray set: gray; clear: colour, the texture code
+    // exactly as before -- a run-time test cost colour captures 1.4 %, profiles/r4r); the generic
+    // instance tests each view.
+    const bool gray = (PLAN & kPlanGray) != 0 || ((PLAN & 0xff) == 0 && p.texture == nullptr);
+    auto load_tex = [&](uint2 white) {
+      if (gray) {
+        tex[0] = white.x;
+        tex[1] = white.y;
+      } else if (!tail) {
         const uint32_t tq = uint32_t(px0) * 3u;   // n_px * 3 < 2^32 (host: slg_capture checks)
         const uint2 t0 = ld_once8_buf(p.texture, tq), t1 = ld_once8_buf(p.texture, tq + 8u),
                     t2 = ld_once8_buf(p.texture, tq + 16u);
@@ -1733,7 +1744,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       }
     };
     constexpr bool MF = SLG_MASK_FIRST && SRC_FRAMES;
-    if (!SLG_TEX_LATE && !MF) load_tex();
+    if (!SLG_TEX_LATE && !MF) load_tex(make_uint2(0u, 0u));   // (gray needs MF: host check)
     uint32_t valid;
     int col[kPx], row[kPx];
     if constexpr (MF) {
@@ -1744,7 +1755,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     }
     // SLG_TEX_LATE: only lanes with a valid pixel read their 24 texture bytes, once the mask is
     // known (the block scan's barrier covers part of the latency)
-    if (!MF && SLG_TEX_LATE && valid != 0u) load_tex();
+    if (!MF && SLG_TEX_LATE && valid != 0u) load_tex(make_uint2(0u, 0u));
     const int2 sc = block_scan(__popc(valid), s_wtot);
     n_items = sc.y;
     int m = sc.x;
@@ -1754,7 +1765,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     for (int k = 0; k < kPx; ++k) {
       if (valid & (1u << k)) {
         s_item[item_slot(m)] = make_uint2(pack_code<ROW_MODE>(p, col[k], row[k]), uint32_t(u) | (uint32_t(v) << 16));
-        s_bgr[bgr_slot(m)] = bgr_of(tex, k);
+        s_bgr[bgr_slot(m)] = gray ? ((tex[k >> 2] >> (8 * (k & 3))) & 0xffu) * 0x010101u : bgr_of(tex, k);
         ++m;
       }
       if (++u == p.width) { u = 0; ++v; }
@@ -2296,10 +2307,13 @@ Main3Fn pick_main(int row_mode, int x64, int rays, int plan = 0) {
   }
 #ifndef SLG_FAST_BUILD
   if (SRC == 1 && rays == SLG_RAYS_PINHOLE && row_mode != 0) {
-#define SLG_PCASE(RM, X, PL) if (row_mode == RM && x64 == X && plan == PL) return main3_kernel<RM, X, 1, 1, false, PL>;
+#define SLG_PCASE(RM, X, PL) if (row_mode == RM && x64 == X && plan == (PL)) return main3_kernel<RM, X, 1, 1, false, (PL)>;
     SLG_PCASE(1, 0, SLG_PLAN_C2) SLG_PCASE(1, 1, SLG_PLAN_C2)
     SLG_PCASE(1, 0, SLG_PLAN_1080P) SLG_PCASE(1, 1, SLG_PLAN_1080P)
     SLG_PCASE(1, 0, SLG_PLAN_C4) SLG_PCASE(1, 1, SLG_PLAN_C4)
+    SLG_PCASE(1, 0, SLG_PLAN_C2 | kPlanGray) SLG_PCASE(1, 1, SLG_PLAN_C2 | kPlanGray)
+    SLG_PCASE(1, 0, SLG_PLAN_1080P | kPlanGray) SLG_PCASE(1, 1, SLG_PLAN_1080P | kPlanGray)
+    SLG_PCASE(1, 0, SLG_PLAN_C4 | kPlanGray) SLG_PCASE(1, 1, SLG_PLAN_C4 | kPlanGray)
 #undef SLG_PCASE
   }
 #endif
@@ -2356,7 +2370,7 @@ int check_batch(const slg_capture* caps, int n_views) {
   for (int v = 0; v < n_views; ++v) {
     const int rc = check_capture(&caps[v]);
     if (rc) return rc;
-    if (!caps[v].texture) return fail(SLG_ERR_INVALID, "capture %d: texture is NULL", v);
+    if (!caps[v].texture && !SLG_MASK_FIRST) return fail(SLG_ERR_INVALID, "capture %d: texture is NULL", v);
     if (reinterpret_cast<uintptr_t>(caps[v].texture) & 7) return fail(SLG_ERR_INVALID, "texture must be 8-byte aligned");
     if (caps[v].height != caps[0].height || caps[v].width != caps[0].width)
       return fail(SLG_ERR_INVALID, "all views of a batch must share one geometry");
@@ -2408,12 +2422,17 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
   for (int v0 = 0, launch = 0; v0 < n_views; v0 += kMaxViews, ++launch) {
     mp.n_views = n_views - v0 < kMaxViews ? n_views - v0 : kMaxViews;
     int plan = -1;                                  // the views' common pair counts, else 0
+    bool all_gray = true, any_gray = false;         // gray captures (texture NULL)
     for (int k = 0; k < mp.n_views; ++k) {
       Plan pl;
       make_plan(&caps[v0 + k], dp, &pl);
       const int key = pl.col_pairs <= 15 && pl.row_pairs <= 15 ? (pl.col_pairs << 4) | pl.row_pairs : 0;
       plan = plan < 0 || plan == key ? key : 0;
+      all_gray = all_gray && !caps[v0 + k].texture;
+      any_gray = any_gray || !caps[v0 + k].texture;
     }
+    // a mixed launch runs the generic instance (per-view test); a plan instance is all one kind
+    if (plan > 0 && any_gray) plan = all_gray ? (plan | kPlanGray) : 0;
     const Main3Fn fn = pick_main<1>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode, plan < 0 ? 0 : plan);
     for (int k = 0; k < mp.n_views; ++k) {
       const int v = v0 + k;

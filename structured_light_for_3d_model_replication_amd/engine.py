@@ -50,12 +50,19 @@ def weak_scalar(x) -> float:
 
 
 # ----------------------------------------------------------------------------- frames
+GRAY = "gray"       # DeviceFrames texture mode: BGR = frame 0 replicated, never materialised
+
+
 class DeviceFrames:
     """A capture's frame stack in HBM (``uint8 [F, stride]``) plus its BGR texture."""
 
     def __init__(self, frames, texture=None, device=None, n_frames=None):
         """``frames``: uint8 tensor [F,H,W] (any device) or a sequence of HxW arrays in capture
-        order; ``None`` entries are frames the decode will not read (left unset in HBM)."""
+        order; ``None`` entries are frames the decode will not read (left unset in HBM).
+        ``texture``: BGR [H,W,3]; ``None``: frame 0 replicated, stored; :data:`GRAY`: frame 0
+        replicated, not stored -- the fused kernels take the colour from the white bytes they
+        read anyway (``slg_capture.texture`` NULL), what ``cv2.imread(files[0])`` of an 8-bit
+        gray PNG capture gives."""
         device = device or default_device()
         if isinstance(frames, torch.Tensor) and frames.dim() == 3:
             F, H, W = frames.shape
@@ -81,6 +88,11 @@ class DeviceFrames:
                 if a.size != self.n_px:
                     raise ValueError("all frames must have the same size")
                 self.data[k, : self.n_px].copy_(torch.from_numpy(a))
+        if isinstance(texture, str):
+            if texture != GRAY:
+                raise ValueError(f"texture mode must be {GRAY!r}")
+            self.texture = None
+            return
         if texture is None:
             t0 = frames[0] if frames_iter is None else frames_iter[0]
             t0 = t0.cpu().numpy() if isinstance(t0, torch.Tensor) else np.asarray(t0)
@@ -92,22 +104,35 @@ class DeviceFrames:
             self.texture = torch.from_numpy(tex).to(device)
 
     @classmethod
-    def allocate(cls, n_frames: int, height: int, width: int, device=None) -> "DeviceFrames":
+    def allocate(cls, n_frames: int, height: int, width: int, device=None, gray: bool = False) -> "DeviceFrames":
         """Uninitialised stack + texture of this layout, for a caller that fills them itself
-        (the batch file pipeline: async H2D from pinned host memory, device-side texture)."""
+        (the batch file pipeline: async H2D from pinned host memory, device-side texture);
+        ``gray``: no texture buffer (:data:`GRAY` mode)."""
         self = cls.__new__(cls)
         device = device or default_device()
         self.height, self.width, self.n_px = int(height), int(width), int(height) * int(width)
         self.n_frames = int(n_frames)
         self.stride = (self.n_px + 15) // 16 * 16
         self.data = torch.empty((max(self.n_frames, 2), self.stride), dtype=torch.uint8, device=device)
-        self.texture = torch.empty((self.n_px, 3), dtype=torch.uint8, device=device)
+        self.texture = None if gray else torch.empty((self.n_px, 3), dtype=torch.uint8, device=device)
         return self
 
     def capture(self) -> N.Capture:
         return N.Capture(frames=self.data.data_ptr(), frame_stride=self.stride,
                          n_frames=self.n_frames, height=self.height, width=self.width,
-                         reserved=0, texture=self.texture.data_ptr())
+                         reserved=0, texture=self.texture.data_ptr() if self.texture is not None else 0)
+
+    def texture_bgr(self) -> torch.Tensor:
+        """The BGR texture [n_px, 3] as a device tensor; a :data:`GRAY` capture's is made from
+        frame 0 (``slg_gray_texture``) on the current stream, for the callers that return or
+        gather it."""
+        if self.texture is not None:
+            return self.texture
+        t = torch.empty((self.n_px, 3), dtype=torch.uint8, device=self.data.device)
+        N.check(N.lib().slg_gray_texture(ctypes.c_void_p(self.data.data_ptr()), self.n_px,
+                                         ctypes.c_void_p(t.data_ptr()),
+                                         ctypes.c_void_p(torch.cuda.current_stream(self.data.device).cuda_stream)))
+        return t
 
 
 # ----------------------------------------------------------------------------- calibration

@@ -57,9 +57,11 @@ def stage_copies(sources, plan, device=None):
     out = []
     for j, s in enumerate(plan):
         src = sources[s]
-        d = E.DeviceFrames.allocate(src.n_frames, src.height, src.width, device=device or src.data.device)
+        d = E.DeviceFrames.allocate(src.n_frames, src.height, src.width, device=device or src.data.device,
+                                    gray=src.texture is None)
         d.data.copy_(src.data)
-        d.texture.copy_(src.texture)
+        if src.texture is not None:
+            d.texture.copy_(src.texture)
         out.append(d)
     return out
 

@@ -92,9 +92,10 @@ def _decode_rgb(path) -> np.ndarray:
 
 def device_png_enabled() -> bool:
     """PNG captures decoded on the GPU (``slg_png_decode_device``) with SLG_PNG_DEVICE=1; off by
-    default: the inflate is one wave per stream at ~0.5 s per 1080p frame, so even 16 views per
-    launch (704 streams) take 30 ms per view against 20 ms for the host decoder on the box's 16
-    CPUs (profiles/r4i).  Correct and tested (tests/test_png_device.py), kept for hosts with
+    default.  The inflate is one wave per stream, ~225 ms per 1080p frame, so it needs 16 views
+    per launch (704 streams) to reach 14 ms per view against 20 ms for the host decoder on the
+    box's 16 CPUs, and in this pipeline the host decoder gives the lower s/view (DESIGN §4,
+    profiles/r4n, r4o).  Correct and tested (tests/test_png_device.py), kept for hosts with
     fewer CPUs per GPU."""
     return os.environ.get("SLG_PNG_DEVICE", "0") == "1" and not os.environ.get("SLG_PNG_PIL")
 
@@ -203,14 +204,22 @@ def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", 
                     weights=weights, pinned=[buf])
 
 
+def _gray_mode(hv: HostView) -> bool:
+    """Whether a HostView's texture is its frame 0 replicated (gray stack without an explicit
+    texture, or a one-channel PNG for the device decoder): the GRAY texture mode."""
+    return (hv.kind == "gray" and hv.texture is None) or (hv.kind == "png_z" and hv.channels == 1)
+
+
 def upload_views(hvs, stream) -> list:
-    """Async H2D of HostViews on ``stream`` (pinned sources) + the device textures: frame 0
-    replicated for gray captures, frame 0's BGR for colour ones (``slg_gray_texture`` /
-    ``slg_rgb_to_gray``).  The PNG captures (kind "png_z") of the list are decoded by ONE
+    """Async H2D of HostViews on ``stream`` (pinned sources) + the device textures: none for
+    gray captures (GRAY mode: the kernels take frame 0), frame 0's BGR for colour ones
+    (``slg_rgb_to_gray``).  The PNG captures (kind "png_z") of the list are decoded by ONE
     ``slg_png_decode_device`` launch over all their frames (a view's 44 streams alone leave the
     GPU nearly idle: the decode is one wave per stream).  The host buffers must stay alive until
     ``stream`` reaches here.  Returns the DeviceFrames in order."""
-    devs = [E.DeviceFrames.allocate(hv.n_files, hv.height, hv.width) for hv in hvs]
+    # gray captures whose texture is frame 0 (the 8-bit gray PNGs the reference's scanner writes)
+    # run in GRAY texture mode: no texture buffer, the kernels take the colour from frame 0
+    devs = [E.DeviceFrames.allocate(hv.n_files, hv.height, hv.width, gray=_gray_mode(hv)) for hv in hvs]
     sp = ctypes.c_void_p(stream.cuda_stream)
     L = N.lib()
     with torch.cuda.stream(stream):
@@ -222,9 +231,6 @@ def upload_views(hvs, stream) -> list:
                 dev.data[: hv.n_files].copy_(hv.stack, non_blocking=True)
                 if hv.texture is not None:
                     dev.texture.copy_(hv.texture, non_blocking=True)
-                else:
-                    N.check(L.slg_gray_texture(ctypes.c_void_p(dev.data.data_ptr()), dev.n_px,
-                                               ctypes.c_void_p(dev.texture.data_ptr()), sp))
             elif hv.kind == "rgb":
                 rgb = torch.empty(hv.stack.shape, dtype=torch.uint8, device=dev.data.device)
                 rgb.copy_(hv.stack, non_blocking=True)
@@ -276,8 +282,7 @@ def decode_png_device(pngs, stream) -> None:
     N.check(L.slg_png_decode_device(ctypes.c_void_p(ddev.data_ptr()), n_all, ctypes.c_void_p(status.data_ptr()), sp))
     for hv, dev, rgb in keep:
         if rgb is None:
-            N.check(L.slg_gray_texture(ctypes.c_void_p(dev.data.data_ptr()), dev.n_px,
-                                       ctypes.c_void_p(dev.texture.data_ptr()), sp))
+            pass                                         # gray: GRAY texture mode (frame 0)
         else:
             N.check(L.slg_rgb_to_gray(ctypes.c_void_p(rgb.data_ptr()), hv.channels, dev.n_px, rgb.shape[1],
                                       hv.n_files, ctypes.c_void_p(dev.data.data_ptr()), dev.stride,

@@ -217,7 +217,18 @@ def load_capture(source, cfg: E.DecodeConfig, order=("bmp", "png"), host=None):
     """Discover, decode and upload one capture: ``(DeviceFrames, texture)``.  ``host``: the
     result of :func:`read_capture` when it was already done (e.g. prefetched)."""
     stack, texture = host if host is not None else read_capture(source, cfg, order)
-    return E.DeviceFrames(stack, texture), texture
+    return E.DeviceFrames(stack, E.GRAY if _is_frame0(texture, stack) else texture), texture
+
+
+def _is_frame0(texture, stack) -> bool:
+    """Whether the BGR texture is frame 0 replicated (an 8-bit gray capture): the device copy
+    then runs in GRAY texture mode and the texture is never uploaded."""
+    t = np.asarray(texture)
+    f0 = stack[0]
+    if f0 is None or t.ndim != 3 or t.shape[2] != 3:
+        return False
+    f0 = np.asarray(f0)
+    return t.shape[:2] == f0.shape and all(np.array_equal(t[..., c], f0) for c in range(3))
 
 
 class ProcessingLogic:
@@ -238,7 +249,7 @@ class ProcessingLogic:
                              contrast_val, "processing")
         if isinstance(source, E.DeviceFrames):
             dev = source
-            texture = source.texture.reshape(dev.height, dev.width, 3).cpu().numpy()
+            texture = source.texture_bgr().reshape(dev.height, dev.width, 3).cpu().numpy()
         elif isinstance(source, (np.ndarray, torch.Tensor)) and source.ndim == 3:
             dev = E.DeviceFrames(source)
             texture = dev.texture.reshape(dev.height, dev.width, 3).cpu().numpy()

@@ -79,7 +79,7 @@ class SLSystem:
         print("Reconstructing 3D points...")
         print(f"Processing {int(mask.sum().item())} valid pixels...")
         dc = PR._device_calib(calib_data, dev.height, dev.width)
-        P, C = eng.triangulate(col, row, mask, dev.texture, dc, row_mode=0, xyz_f64=True).result()
+        P, C = eng.triangulate(col, row, mask, dev.texture_bgr(), dc, row_mode=0, xyz_f64=True).result()
         points, colors = P.cpu().numpy(), C.cpu().numpy()
 
         ply_name = os.path.basename(scan_dir) + ".ply"

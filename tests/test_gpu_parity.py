@@ -667,3 +667,37 @@ def test_device_ply_body_matches_host_formatter(tmp_path, mods):
         P = pts[:5].copy()
         P[3, 1] = bad
         assert fmt.body(torch.from_numpy(P).cuda(), torch.from_numpy(cols[:5]).cuda()) is None, bad
+
+
+@pytest.mark.parametrize("name", ["proc_otsu_full", "proc_c2style", "proc_odd_geometry", "sl_full"])
+def test_gray_texture_mode_matches_materialised(name, mods):
+    """GRAY texture mode (slg_capture.texture NULL: the colour of a point is frame 0 replicated,
+    taken from the white bytes the kernel reads anyway) == the same capture with that texture
+    stored and read, bitwise, for every row mode, f64 and f32, one-view and batched launches
+    (ragged 101x37 geometry: the tail tile's guarded path)."""
+    E, PR, N = mods
+    z = load_case(name)
+    cal = load_calibs()[z["params"]["calib"]]
+    frames = list(z["frames"])
+    tex = np.repeat(np.asarray(frames[0])[..., None], 3, axis=-1)
+    stored = E.DeviceFrames(frames, tex)
+    gray = E.DeviceFrames(frames, E.GRAY)
+    assert gray.texture is None and gray.capture().texture in (0, None)
+    assert np.array_equal(gray.texture_bgr().cpu().numpy(), stored.texture.cpu().numpy())
+    eng = E.Reconstructor(stored.height, stored.width)
+    dc = E.DeviceCalib(cal, stored.height, stored.width)
+    cfg = _cfg(E, z["params"])
+    for rm in (0, 1, 2):
+        for f64 in (True, False):
+            a = [t.cpu().numpy() for t in eng.reconstruct(stored, cfg, dc, row_mode=rm, xyz_f64=f64).result()]
+            b = [t.cpu().numpy() for t in eng.reconstruct(gray, cfg, dc, row_mode=rm, xyz_f64=f64).result()]
+            assert len(a[0]) > 0 and np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), (rm, f64)
+    beng = E.BatchReconstructor(stored.height, stored.width, 3)
+    clouds = {k: [E.Cloud(stored.n_px, 1, True) for _ in range(3)] for k in ("s", "g")}
+    outs = {}
+    for k, views in (("s", [stored, gray, stored]), ("g", [gray, gray, gray])):
+        pb = beng.prepare(views, cfg, dc, clouds[k], 1)
+        beng.run(pb)
+        outs[k] = [[t.cpu().numpy() for t in c.result()] for c in clouds[k]]
+    for (pa, ca), (pg, cg) in zip(outs["s"], outs["g"]):
+        assert np.array_equal(pa, pg) and np.array_equal(ca, cg)
