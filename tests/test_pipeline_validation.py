@@ -111,3 +111,28 @@ def test_packed_clouds_keep_the_capacity_contract():
     assert x64.dtype == torch.float64
     with pytest.raises(ValueError):
         J.packed_clouds(n_px, [3, -1], device="cpu")
+
+
+def test_gray_texture_mode_selection():
+    """Which captures run in GRAY texture mode (no texture buffer; slg_capture.texture NULL): a
+    texture equal to frame 0 replicated (what cv2.imread(files[0]) gives for an 8-bit gray PNG),
+    a gray HostView without an explicit texture, a one-channel PNG for the device decoder; a
+    colour texture, a colour stack or an RGB PNG never."""
+    import numpy as np
+    import torch
+    from structured_light_for_3d_model_replication_amd import pipeline as PL, processing as PR
+    rng = np.random.default_rng(0)
+    f0 = rng.integers(0, 256, (5, 7), dtype=np.uint8)
+    stack = [f0, None, rng.integers(0, 256, (5, 7), dtype=np.uint8)]
+    assert PR._is_frame0(np.repeat(f0[..., None], 3, -1), stack)
+    tinted = np.repeat(f0[..., None], 3, -1)
+    tinted[2, 3, 1] ^= 1
+    assert not PR._is_frame0(tinted, stack)
+    assert not PR._is_frame0(np.repeat(f0[..., None], 3, -1)[:4], stack)
+    assert not PR._is_frame0(np.repeat(f0[..., None], 3, -1), [None, f0])
+    t = torch.zeros(1)
+    hv = lambda kind, ch=1, tex=None: PL.HostView("f", 4, 5, 7, 48, kind, t, channels=ch, texture=tex)
+    assert PL._gray_mode(hv("gray"))
+    assert not PL._gray_mode(hv("gray", tex=torch.zeros(35, 3)))
+    assert PL._gray_mode(hv("png_z", 1)) and not PL._gray_mode(hv("png_z", 3))
+    assert not PL._gray_mode(hv("rgb", 3))
