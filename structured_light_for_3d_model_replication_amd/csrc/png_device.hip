@@ -170,13 +170,14 @@ __device__ inline int decode(Bits& b, const Huff& h) {
   return int(r & 0xffffu);
 }
 
-// Literal runs: lit4[i] holds the literals that the 10 stream bits i decode to in a row, as long
-// as each code fits the bits still known (up to 4: bytes in bits 0-31, count in 32-35, bits used
-// in 36-39); a count of 0 (the first code is a length / end-of-block symbol, or longer than
-// 10 bits) falls back to decode().  PNG scanline residuals code in ~4 bits a byte, so one LDS
+// Literal runs: lit4[i] holds the literals that the next kLitBits stream bits i decode to in a
+// row, as long as each code fits the bits still known (at most kLitMax), with their count and the
+// bits they use; a count of 0 (the first code is a length / end-of-block symbol, or longer than
+// kFastBits) falls back to decode().  PNG scanline residuals code in ~4 bits a byte, so one LDS
 // lookup on the serial chain yields ~2.5 literals instead of one.
 #ifndef PNG_LIT11
-#define PNG_LIT11 1                          // 11-bit index, 4-byte entries, <= 3 literals: 14.07 vs 16.28 ms/view (10-bit, 8-byte, <= 4; profiles/r4n)
+#define PNG_LIT11 1   // 11-bit index, 4-byte entries, <= 3 literals: 14.07 vs 16.28 ms/view for the
+                      // 10-bit, 8-byte, <= 4 form (profiles/r4n/png_lit11_ab.log)
 #endif
 #if PNG_LIT11
 constexpr int kLitBits = 11, kLitMax = 3;
@@ -395,7 +396,7 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
       const LitEntry e4 = L.lit4[uint32_t(b.buf) & ((1u << kLitBits) - 1u)];
       const uint32_t cu = uni(uint32_t(e4 >> kLitCountShift));
       const uint32_t n4 = cu & 15u;
-      if (n4) {                                              // a run of 1-4 literals
+      if (n4) {                                              // a run of 1..kLitMax literals
         const uint32_t used = (cu >> 4) & 15u;
         b.buf >>= used;
         b.cnt -= int(used);
