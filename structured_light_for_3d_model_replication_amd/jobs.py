@@ -15,8 +15,9 @@ MI355X's HBM.  :class:`ResidentJob` runs such a job with every view already resi
   points of slack, so from any view's start there are at least ``H*W`` points to the arena's end
   -- the C ABI's capacity contract (``slg_cloud.capacity >= H*W``) holds for every view and no
   store can leave the allocation.  A view whose count exceeds its hint has written into its
-  successor's region: :meth:`ResidentJob.overflowed` names such views (re-run them into a cloud
-  of their own).  With exact hints (a previous pass over the same frames, or per-view valid-pixel
+  successors' regions: :meth:`ResidentJob.overflowed` names such views, and
+  :meth:`ResidentJob.damaged` adds the views whose region an overflow reached (re-run all of
+  them into clouds of their own).  With exact hints (a previous pass over the same frames, or per-view valid-pixel
   counts) 576 4K clouds take 41 GB instead of the 72 GB of worst-case slots.
 """
 from __future__ import annotations
@@ -108,6 +109,17 @@ class ResidentJob:
         """Views whose cloud ran past their capacity hint (into the next view's region)."""
         counts = self.host_counts() if counts is None else counts
         return [j for j, (n, h) in enumerate(zip(counts, self.hints)) if n > h]
+
+    def damaged(self, counts=None):
+        """Views whose cloud cannot be trusted: the overflowed ones and every later view whose
+        region starts before an overflowed view's last point (its points may be overwritten)."""
+        counts = self.host_counts() if counts is None else counts
+        bad = set()
+        for j in self.overflowed(counts):
+            bad.add(j)
+            end = self.offsets[j] + counts[j]
+            bad.update(k for k in range(j + 1, len(self.hints)) if self.offsets[k] < end)
+        return sorted(bad)
 
     def cloud(self, j, counts=None):
         """``(xyz, bgr)`` of view j (device slices of the arena)."""

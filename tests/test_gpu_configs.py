@@ -213,7 +213,7 @@ def test_c5_resident_job(mods):
     fused launch per view on the two-stream carried pipeline (4 primed + 4 carried groups), the
     clouds packed in one arena by capacity hints.  Every view's count and colours equal the
     oracle's, XYZ within the north-star tolerance; a view given too small a hint is reported as
-    overflowed (its stores stay inside the arena)."""
+    overflowed and its successor as damaged (the stores stay inside the arena)."""
     E, N = mods
     import torch
     from structured_light_for_3d_model_replication_amd import jobs as J, synth
@@ -250,3 +250,4 @@ def test_c5_resident_job(mods):
     job2.run(s0, s1)
     torch.cuda.synchronize()
     assert job2.overflowed() == [2]
+    assert job2.damaged() == [2, 3]                     # view 3's region begins inside view 2's overflow

@@ -136,3 +136,15 @@ def test_gray_texture_mode_selection():
     assert not PL._gray_mode(hv("gray", tex=torch.zeros(35, 3)))
     assert PL._gray_mode(hv("png_z", 1)) and not PL._gray_mode(hv("png_z", 3))
     assert not PL._gray_mode(hv("rgb", 3))
+
+
+def test_resident_job_damage_reaches_every_overwritten_view():
+    """A packed job view that outgrows its hint overwrites the start of each later view whose
+    region begins before its last point: those are damaged too (jobs.ResidentJob.damaged)."""
+    from structured_light_for_3d_model_replication_amd import jobs as J
+    job = J.ResidentJob.__new__(J.ResidentJob)
+    job.hints = [10, 5, 5, 20, 8]
+    job.offsets = [0, 10, 15, 20, 40, 48]
+    assert job.damaged([10, 5, 5, 20, 8]) == [] and job.overflowed([10, 5, 5, 20, 8]) == []
+    assert job.overflowed([16, 5, 5, 20, 8]) == [0] and job.damaged([16, 5, 5, 20, 8]) == [0, 1, 2]
+    assert job.damaged([10, 5, 6, 20, 9]) == [2, 3, 4]      # 15 + 6 > 20; the last view has no successor
