@@ -395,6 +395,8 @@ def main():
         if getattr(args, k) is None:
             setattr(args, k, wl[k])
     args.result_out = RESULT_OUT         # (bench_c3 imports this file as module "bench")
+    if args.gray_texture and args.config in ("c3", "c5job"):
+        raise SystemExit("--gray-texture applies to the single-view configs (c2, c4, c5)")
     if args.config == "c3":
         import bench_c3
         return bench_c3.main(args, wl)

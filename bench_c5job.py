@@ -138,6 +138,7 @@ def main(args, wl):
         same = all(torch.equal(job.cloud(j, counts)[0], first[plan[j]][0]) and
                    torch.equal(job.cloud(j, counts)[1], first[plan[j]][1]) for j in range(n_views))
         verify = {"views": n_views, "counts_equal_first_pass": counts == hints, "overflowed": over,
+                  "damaged": job.damaged(counts),
                   "clouds_equal_first_pass_bitwise": bool(same)}
         if rank == 0:
             from oracle import sl_oracle as O
