@@ -640,16 +640,16 @@ def main():
                                 else "HIP events around the timed region (both launch streams joined) / steps: "
                                      "the step period, gaps included"),
                 "alg_bytes_per_launch": round(dense_sum / launches),
-                "alg_bytes": ("SURVEY 8(d): (2 + 2(nc+nr)) B per pixel (every frame once) + 18 B per point "
-                              "(3 B texture read, 12 B XYZ, 3 B BGR written)" if not args.gray_texture else
-                              "SURVEY 8(d) without the texture read: (2 + 2(nc+nr)) B per pixel + 15 B per point "
-                              "(12 B XYZ, 3 B BGR written; a gray capture's colour is its white frame)"),
+                "alg_bytes": (f"SURVEY 8(d): (2 + 2(nc+nr)) B per pixel (every frame once) + {out_b} B per point "
+                              f"(3 B texture read, {24 if f64 else 12} B XYZ, 3 B BGR written)" if not args.gray_texture else
+                              f"SURVEY 8(d) without the texture read: (2 + 2(nc+nr)) B per pixel + {out_b} B per point "
+                              f"({24 if f64 else 12} B XYZ, 3 B BGR written; a gray capture's colour is its white frame)"),
                 # the kernel reads a pattern frame only where a lane holds a valid pixel (SLG_MASK_FIRST),
                 # so it moves fewer bytes than SURVEY's figure: the same time over the bytes it needs
                 "mask_first": {"alg_bytes_per_launch": round(bytes_sum / launches),
                                "achieved": round(mf_achieved, 1), "frac": round(mf_achieved / HBM_PEAK_GBS, 4),
                                "what": "white + black of every pixel, each pattern frame's 64-B segments that hold "
-                                       "a valid pixel, 18 B per point"}}
+                                       f"a valid pixel, {out_b} B per point"}}
         out = {
             "metric": METRIC,
             "value": round(all_pts / dt_max / 1e6, 2),
