@@ -250,8 +250,12 @@ __device__ __attribute__((noinline)) bool build(Huff& h, const uint8_t* lens, in
   return !bad;
 }
 
+#ifndef PNG_LIT_WORD
+#define PNG_LIT_WORD 1                       // literal runs stored as one unaligned LDS word by lane 0
+#endif
+
 struct InflateLds {
-  alignas(16) uint8_t ring[kRing];
+  alignas(16) uint8_t ring[kRing + 4];    // + 4 slack bytes: a literal-run word at the ring's end
   LitEntry lit4[1 << kLitBits];
   Huff lit, dist;
   uint8_t lens[320];                      // litlen code lengths at [0, 288), distance at [288, 320)
@@ -401,11 +405,25 @@ __global__ __launch_bounds__(64) void png_inflate_kernel(const slg_png_frame* fr
         b.buf >>= used;
         b.cnt -= int(used);
         if (pos + int32_t(n4) > n_out) { err = SLG_PNG_E_SIZE; break; }
+#if PNG_LIT_WORD
+        // lane 0 stores the run as one unaligned LDS word (bytes past the run land on positions
+        // not yet written, or in the ring's 4 slack bytes); a run that wraps also writes its
+        // wrapped bytes at the ring's start (rare)
+        if (lane == 0 && !(PNG_ABL & 1)) {
+          const uint32_t word = uint32_t(e4);
+          __builtin_memcpy(&L.ring[ridx], &word, 4);
+        }
+        if (__builtin_expect(ridx + int(n4) > kRing, 0)) {   // (uniform: a scalar branch)
+          __builtin_amdgcn_wave_barrier();
+          if (lane < int(n4) && ridx + lane >= kRing) L.ring[ridx + lane - kRing] = uint8_t(uint32_t(e4) >> (8 * lane));
+        }
+#else
         if (lane < int(n4) && !(PNG_ABL & 1)) {              // lane k writes literal k
           int r = ridx + lane;
           if (r >= kRing) r -= kRing;
           L.ring[r] = uint8_t(uint32_t(e4) >> (8 * lane));
         }
+#endif
         pos += int32_t(n4);
         ridx += int(n4);
         if (ridx >= kRing) ridx -= kRing;

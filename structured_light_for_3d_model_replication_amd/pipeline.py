@@ -93,7 +93,7 @@ def _decode_rgb(path) -> np.ndarray:
 def device_png_enabled() -> bool:
     """PNG captures decoded on the GPU (``slg_png_decode_device``) with SLG_PNG_DEVICE=1; off by
     default.  The inflate is one wave per stream, ~225 ms per 1080p frame, so it needs 16 views
-    per launch (704 streams) to reach 14 ms per view against 20 ms for the host decoder on the
+    per launch (704 streams) to reach 13.8 ms per view against 20 ms for the host decoder on the
     box's 16 CPUs, and in this pipeline the host decoder gives the lower s/view (DESIGN §4,
     profiles/r4n, r4o).  Correct and tested (tests/test_png_device.py), kept for hosts with
     fewer CPUs per GPU."""
