@@ -50,17 +50,22 @@ def log(*a):
 
 
 # Workloads (BASELINE.json configs / SURVEY §8(d)).  c2 is the metric's configuration and the
-# default; the others run on request (--config).
+# default; the others run on request (--config).  A fused2 launch k decodes batch k and carries
+# batch k+4's histograms; with D distinct batches in the pool (views x copies / batch) those are
+# the frames of batch (k+4) mod D.  D = 6 (c4, c5) makes them the batch decoded two launches
+# earlier on the same stream, GBs of traffic ago: cold HBM reads.  (D = 2 or 4 would make them
+# the batch this launch decodes, read twice through the caches.)  c2 keeps D = 3, its measured
+# traffic matching the cold-read model (profiles/r4fin2).
 CONFIGS = {
     "c2": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 10), n_present=44, views=12, copies=4, batch=16,
                text="C2: 1920x1080 view, 11 col + 10 row Gray bits + inverses + white/black (44 frames)"),
     "c3": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 11), n_present=None, views=36, copies=1, batch=12,
                text="C3: 36-view 360-degree turntable scan at 1920x1080, 11 col + 11 row Gray bits + "
                     "inverses + white/black (46 frames), views sharded over the ranks, clouds gathered to rank 0"),
-    "c4": dict(cam=(6000, 4000), proj=(3840, 2160), nsets=(12, 12), n_present=None, views=2, copies=2, batch=2,
+    "c4": dict(cam=(6000, 4000), proj=(3840, 2160), nsets=(12, 12), n_present=None, views=2, copies=6, batch=2,
                text="C4: 6000x4000 view, projector 3840x2160, 12 col + 12 row Gray bits + inverses + "
                     "white/black (50 frames)"),
-    "c5": dict(cam=(3840, 2160), proj=(1920, 1080), nsets=(11, 11), n_present=None, views=4, copies=2, batch=4,
+    "c5": dict(cam=(3840, 2160), proj=(1920, 1080), nsets=(11, 11), n_present=None, views=4, copies=6, batch=4,
                text="C5: 3840x2160 view, projector 1920x1080, 11 col + 11 row Gray bits + inverses + "
                     "white/black (46 frames)"),
     "c5job": dict(cam=(3840, 2160), proj=(1920, 1080), nsets=(11, 11), n_present=None, views=576, copies=1, batch=4,
