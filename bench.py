@@ -52,12 +52,12 @@ def log(*a):
 # Workloads (BASELINE.json configs / SURVEY §8(d)).  c2 is the metric's configuration and the
 # default; the others run on request (--config).  A fused2 launch k decodes batch k and carries
 # batch k+4's histograms; with D distinct batches in the pool (views x copies / batch) those are
-# the frames of batch (k+4) mod D.  D = 6 (c4, c5) makes them the batch decoded two launches
+# the frames of batch (k+4) mod D.  D = 6 (c2, c4, c5) makes them the batch decoded two launches
 # earlier on the same stream, GBs of traffic ago: cold HBM reads.  (D = 2 or 4 would make them
-# the batch this launch decodes, read twice through the caches.)  c2 keeps D = 3, its measured
-# traffic matching the cold-read model (profiles/r4fin2).
+# the batch this launch decodes, read twice through the caches; c2's earlier D = 3 made them the
+# batch the other stream decodes at the same time: 1.7 % faster, profiles/r4ab.)  c2: D = 6 too.
 CONFIGS = {
-    "c2": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 10), n_present=44, views=12, copies=4, batch=16,
+    "c2": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 10), n_present=44, views=12, copies=8, batch=16,
                text="C2: 1920x1080 view, 11 col + 10 row Gray bits + inverses + white/black (44 frames)"),
     "c3": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 11), n_present=None, views=36, copies=1, batch=12,
                text="C3: 36-view 360-degree turntable scan at 1920x1080, 11 col + 11 row Gray bits + "
