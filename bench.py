@@ -57,6 +57,13 @@ def log(*a):
 # the batch this launch decodes, read twice through the caches; c2's earlier D = 3 made them the
 # batch the other stream decodes at the same time: 1.7 % faster, profiles/r4ab.)  c2: D = 6 too.
 CONFIGS = {
+    # c1: the reference GUI's legacy single-view call, _gray_decode(files, n_cols=1024, n_rows=1080)
+    # with the default n_sets (col bits clamp to Bc = 10), row frames absent, row_mode 0
+    # (server/processing.py:28,80-84,174-182)
+    "c1": dict(cam=(1280, 720), proj=(1024, 1080), nsets=(11, 11), n_present=22, views=12, copies=8, batch=16,
+               row_mode=0,
+               text="C1: 1280x720 view, projector 1024 wide, 10 col Gray bits + inverses + white/black (22 frames), "
+                    "row frames absent"),
     "c2": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 10), n_present=44, views=12, copies=8, batch=16,
                text="C2: 1920x1080 view, 11 col + 10 row Gray bits + inverses + white/black (44 frames)"),
     "c3": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 11), n_present=None, views=36, copies=1, batch=12,
@@ -76,6 +83,24 @@ CONFIGS = {
 REF_CALIBRATION_OF = {"c5job": "c5"}     # workloads timed by tools/ref_vs_port.py under another name
 
 
+def row_mode_of(wl) -> int:
+    return int(wl.get("row_mode", 1))
+
+
+def frames_used(wl) -> int:
+    """Frames the decode reads per view: white + black + the used (pattern, inverse) pairs that
+    are present ((2 + 2 (nc + nr)) per pixel; C1 has no row frames)."""
+    from structured_light_for_3d_model_replication_amd import synth
+    (PW, PH), (nc, nr) = wl["proj"], wl["nsets"]
+    bc, br = synth.n_bits(PW), synth.n_bits(PH)
+    used = 2 + 2 * (min(nc, bc) + min(nr, br))
+    row_first = 2 + 2 * bc                     # row bit planes start here whatever nc is
+    present = wl["n_present"] if wl["n_present"] is not None else synth.frame_slots(PW, PH)
+    if present <= row_first:                   # no row frame present: only the column pairs count
+        return min(present, 2 + 2 * min(nc, bc))
+    return min(used, 2 + 2 * min(nc, bc) + (present - row_first))
+
+
 # ----------------------------------------------------------------------------- CPU baseline
 _CPU_JOB = None     # (views, calib, proj, nsets): inherited by the forked workers, never pickled
 MAX_CPU_WORKERS = 64        # host-memory bound of the pool (~1 GB per C2 worker, ~4 at 4K)
@@ -87,14 +112,14 @@ def _cpu_worker(args):
     os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import sl_refseq as R
     seconds, first = args
-    views, cal, proj, nsets = _CPU_JOB
+    views, cal, proj, nsets, row_mode = _CPU_JOB
     (PW, PH), (nc, nr) = proj, nsets
     done, pts, t0 = 0, 0, time.perf_counter()
     while True:
         v = views[(first + done) % len(views)]
         col, row, mask, tex = R.gray_decode(list(v.frames), v.texture, n_cols=PW, n_rows=PH, n_sets_col=nc,
                                             n_sets_row=nr)
-        P, _ = R.reconstruct(col, row, mask, tex, cal, row_mode=1)
+        P, _ = R.reconstruct(col, row, mask, tex, cal, row_mode=row_mode)
         pts += len(P)
         done += 1
         if time.perf_counter() - t0 >= seconds:
@@ -168,7 +193,7 @@ def cpu_baseline(views, cal, seconds, wl, config: str):
     global _CPU_JOB
     import numpy as np
     cal = dict(cal, Nc=np.asfortranarray(cal["Nc"]))
-    _CPU_JOB = (views, cal, wl["proj"], wl["nsets"])
+    _CPU_JOB = (views, cal, wl["proj"], wl["nsets"], row_mode_of(wl))
     nsets = wl["nsets"]
     one = _cpu_worker((seconds, 0))
     try:
@@ -187,7 +212,7 @@ def cpu_baseline(views, cal, seconds, wl, config: str):
     tag = wl["text"].split(":")[0]
     return {"value": round(pts / wall / 1e6, 4), "unit": "Mpoints/s", "cores": workers, "kind": "port",
             "sample": f"{n_views} {tag} views ({wl['cam'][0]}x{wl['cam'][1]}, {nsets[0]}+{nsets[1]} bits, Otsu, "
-                      f"row_mode 1) on {workers} worker processes x ~{seconds:.0f} s, frames in memory",
+                      f"row_mode {row_mode_of(wl)}) on {workers} worker processes x ~{seconds:.0f} s, frames in memory",
             "what": "oracle/sl_refseq.py: the reference's NumPy operation sequence for server/processing.py:49-234 "
                     "(in-memory frames, no PNG decode), one view stream per process",
             "ref_calibration": ref_over_port(config),
@@ -445,7 +470,7 @@ def main():
     from structured_light_for_3d_model_replication_amd import engine as E
 
     cfg = E.DecodeConfig(PW, PH, NC, NR, "otsu")
-    row_mode, tol, f64 = 1, 2.0, args.xyz == "f64"
+    row_mode, tol, f64 = row_mode_of(wl), 2.0, args.xyz == "f64"
     # Device pool: every rendered view uploaded `copies` times (distinct HBM buffers), so a batch
     # never shares frames with the batch before or after next -- e.g. the histograms a fused
     # launch computes for batch k+2 are cold HBM reads, as in a real turntable stream.
@@ -496,7 +521,7 @@ def main():
         a.record(s_main)
         b.record(s_main)
     torch.cuda.synchronize()
-    frame_b = (2 + 2 * (NC + NR)) * H * W
+    frame_b = frames_used(wl) * H * W
     out_b = 30 if f64 else 18            # 3 B texture read + 12|24 B XYZ + 3 B BGR per point
     if args.gray_texture:
         out_b -= 3                       # GRAY mode: the colour comes from the white frame, no texture read
@@ -580,7 +605,7 @@ def main():
         v0 = pool_views(last)[0]
         vw = views[v0 % len(views)]
         oc, orow, om = O.decode_processing(list(vw.frames), n_cols=PW, n_rows=PH, n_sets_col=NC, n_sets_row=NR)
-        Po, Co = O.reconstruct_processing(oc, orow, om, vw.texture, cal, row_mode=1)
+        Po, Co = O.reconstruct_processing(oc, orow, om, vw.texture, cal, row_mode=row_mode)
         xg = got[0][1].double().cpu().numpy()
         rel = float(np.max(np.abs(xg - Po) / np.maximum(np.abs(Po), 1e-3))) if len(Po) == len(xg) else None
         oracle_ok = (len(Po) == got[0][0] and np.array_equal(got[0][2].cpu().numpy(), Co)
@@ -609,18 +634,22 @@ def main():
         kern_avg_s = kern_sum / launches / 1e3
         achieved = dense_sum / launches / kern_avg_s / 1e9          # SURVEY 8(d)'s algorithmic bytes
         mf_achieved = bytes_sum / launches / kern_avg_s / 1e9       # the mask-first decode's own bytes
-        pmc = load_traffic_per_view(args.config) if args.config in ("c2", "c4", "c5") else None
-        pmc_name = "pmc_main_kernel.json" if args.config == "c2" else f"pmc_main_kernel_{args.config}.json"
+        # the committed PMC summary of this instance: pmc_main_kernel[_<config>][_f64].json
+        pkey = args.config if not f64 else ("f64" if args.config == "c2" else f"{args.config}_f64")
+        pmc = load_traffic_per_view(pkey) if args.config in ("c1", "c2", "c4", "c5") else None
+        pmc_name = "pmc_main_kernel.json" if pkey == "c2" else f"pmc_main_kernel_{pkey}.json"
         traffic_view = pmc["hbm_bytes_per_view"] if pmc else None
         n_pts_mean = float(np.mean(pts))
         model = {k: round(float(np.mean([m[k] for m in models]))) for k in models[0]}
-        model["writes"] = round(15 * n_pts_mean + 1024 * ((H * W + 4095) // 4096))   # cloud + Otsu partials
+        xyz_b = 24 if f64 else 12
+        model["writes"] = round((xyz_b + 3) * n_pts_mean + 1024 * ((H * W + 4095) // 4096))   # cloud + Otsu partials
         model["total_with_writes"] = model["total"] + model["writes"]
         traffic_model = {"per_view": model,
                          "what": "bytes the fused launch must move per view (pool average) at the 128-B read "
                                  "request size the PMC counters show: white + black, pattern-frame lines holding a "
                                  "valid pixel, texture lines of valid lanes, the carried batch's white + black; "
-                                 "writes 15 B per point (12 B XYZ + 3 B BGR) + 1 KB of Otsu partials per tile"}
+                                 f"writes {xyz_b + 3} B per point ({xyz_b} B XYZ + 3 B BGR) + 1 KB of Otsu partials "
+                                 "per tile"}
         if pmc:
             traffic_model["measured_per_view"] = {"reads": pmc.get("fetch_bytes_per_view"),
                                                   "writes": pmc.get("write_bytes_per_view"),
@@ -638,14 +667,15 @@ def main():
                 "kernel": (f"main3_kernel<1,{int(f64)},1,1,false,PLAN=0x{(0x100 if args.gray_texture else 0) | (NC << 4) | NR:X}> "
                            f"(fused decode+triangulate+"
                            f"compaction, decode-plan instance, {B} views per launch)"
-                           if (NC, NR) in ((11, 10), (11, 11), (12, 12)) else
-                           f"main3_kernel<1,{int(f64)},1,1> (fused decode+triangulate+compaction, {B} views per launch)"),
+                           if (NC, NR) in ((11, 10), (11, 11), (12, 12)) and row_mode == 1 else
+                           f"main3_kernel<{row_mode},{int(f64)},1,1> (fused decode+triangulate+compaction, {B} views per launch)"),
                 "kernel_avg_us": round(kern_avg_s * 1e6, 2),
                 "kernel_time": ("HIP events around each fused launch on its stream" if args.kernel_events == "launch"
                                 else "HIP events around the timed region (both launch streams joined) / steps: "
                                      "the step period, gaps included"),
                 "alg_bytes_per_launch": round(dense_sum / launches),
-                "alg_bytes": (f"SURVEY 8(d): (2 + 2(nc+nr)) B per pixel (every frame once) + {out_b} B per point "
+                "alg_bytes": (f"SURVEY 8(d): (2 + 2(nc+nr)) B per pixel (every frame once; {frames_used(wl)} frames) "
+                              f"+ {out_b} B per point "
                               f"(3 B texture read, {24 if f64 else 12} B XYZ, 3 B BGR written)" if not args.gray_texture else
                               f"SURVEY 8(d) without the texture read: (2 + 2(nc+nr)) B per pixel + {out_b} B per point "
                               f"({24 if f64 else 12} B XYZ, 3 B BGR written; a gray capture's colour is its white frame)"),
@@ -668,7 +698,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"{wl['text']}, Otsu, row_mode 1 tol 2.0, XYZ {args.xyz} + BGR out"
+            "config": {"workload": f"{wl['text']}, Otsu, row_mode {row_mode}"
+                                   + (" tol 2.0" if row_mode == 1 else "") + f", XYZ {args.xyz} + BGR out"
                                    + (", gray capture (texture = frame 0, GRAY mode)" if args.gray_texture else ""),
                        "step": f"one batch of {B} views: one fused launch + its thresholds (steady-state pipeline)",
                        "us_per_view": round(dt_max / (K * B) * 1e6, 3),

@@ -92,6 +92,8 @@ def main(args, wl):
     host_x = host_b = None
     own_x = own_b = None
     own_counts = []
+    d2h_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    d2h_ms = [0.0]                     # this rank's D2H copy time over the timed steps
 
     def reconstruct():
         for pb in preps:
@@ -109,10 +111,12 @@ def main(args, wl):
             own_b = torch.empty((max(1, sum(counts)), 3), dtype=torch.uint8, pin_memory=True)
         off = 0
         with torch.cuda.stream(s):
+            d2h_ev[0].record(s)
             for c, n in zip(clouds, counts):
                 own_x[off:off + n].copy_(c.xyz[:n], non_blocking=True)
                 own_b[off:off + n].copy_(c.bgr[:n], non_blocking=True)
                 off += n
+            d2h_ev[1].record(s)
         own_counts = counts
 
     def gather_step():
@@ -133,7 +137,7 @@ def main(args, wl):
                 host_b[: rb.shape[0]].copy_(rb, non_blocking=True)
         return got
 
-    def timed(fn, k):
+    def timed(fn, k, local=None):
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -141,11 +145,17 @@ def main(args, wl):
         t0 = time.perf_counter()
         for _ in range(k):
             fn()
+            if fn is d2h_step:             # (the step's own sync on its counts orders the events)
+                d2h_ev[1].synchronize()
+                d2h_ms[0] += d2h_ev[0].elapsed_time(d2h_ev[1])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        mine_s = time.perf_counter() - t0
+        if local is not None:
+            local.append(mine_s)
+        dt = torch.tensor([mine_s], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
         return float(dt.item())
@@ -165,12 +175,17 @@ def main(args, wl):
     torch.cuda.synchronize()
     kern_ms = sum(a.elapsed_time(b) for a, b in ev)
 
-    dt = timed(d2h_step, K)
+    local_dt = []
+    d2h_ms[0] = 0.0
+    dt = timed(d2h_step, K, local_dt)
     dt_gather = timed(gather_step, K)
     got = gather_step()
     d2h_step()
     torch.cuda.synchronize()
     counts_local = list(own_counts)
+    # per-rank rows beside the max-over-ranks headline: kernels, D2H, the rank's own step time
+    per_rank = D.per_rank_table({"views": len(mine), "points": sum(counts_local), "kernel_ms": kern_ms,
+                                 "d2h_ms": d2h_ms[0] / K, "step_ms": local_dt[0] / K * 1e3}, device=dev)
     pts_local = torch.tensor([float(sum(counts_local))], dtype=torch.float64, device=dev)
     kern = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -228,6 +243,10 @@ def main(args, wl):
                                                     "there" if gather is not None else
                                                     f"{backend} host gather (rehearsal)")},
                        "batch_views": B,
+                       "per_rank": per_rank,
+                       "per_rank_what": "each rank's views, points, reconstruct kernel ms (HIP events), D2H ms per "
+                                        "step (HIP events around its copies) and own step ms; the headline is the "
+                                        "max over ranks",
                        "parallelism": f"view-sharded x{world}, per-rank D2H"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": bench.HBM_PEAK_GBS, "unit": "GB/s",

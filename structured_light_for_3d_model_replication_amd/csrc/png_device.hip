@@ -104,7 +104,10 @@ struct Bits {
 };
 
 __device__ inline void bits_init(Bits& b, const uint8_t* z, int64_t zlen) {
-  b.rsrc = uni_rsrc(z, uint32_t(zlen));
+  // zlen + 8: slg_png_zstream leaves 8 readable (zeroed) bytes behind every stream, so the dword
+  // holding the stream's last bytes is read whole (with zlen alone, a dword that straddled zlen
+  // would come back 0; only the Adler-32 trailer after the deflate data kept that harmless)
+  b.rsrc = uni_rsrc(z, uint32_t(zlen + 8));
   const int lane = threadIdx.x;
   b.cur = __builtin_amdgcn_raw_buffer_load_b32(b.rsrc, lane * 4, 0, 0);
   b.next = __builtin_amdgcn_raw_buffer_load_b32(b.rsrc, lane * 4, 256, 0);

@@ -25,6 +25,7 @@
 // -ffp-contract=off (no FMA contraction), IEEE-correct f64 division and sqrt, so the fp64
 // results equal the reference bit for bit; integer/byte work is exact by construction.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdarg.h>
@@ -77,12 +78,18 @@ struct WsHeader {
   double thr_s;            // float thresholds (for inspection / tests)
   double thr_c;
   int64_t totals[2];       // column / row stream point totals
-  uint64_t pad3[8];
+  // Otsu only: pixels with white >= smin, and with white - black >= cmin (n_px when cmin <= 0,
+  // which the clipped histogram cannot count); their minimum bounds the valid pixels, so the
+  // point count of row_mode 0/1 (resident jobs size their clouds with it).  n_px otherwise.
+  int64_t above[2];
+  uint64_t pad3[6];
 };
 constexpr int kHistCopies = 16;            // partial histograms: blocks spread their atomics
 constexpr int64_t kHistPartOff = 8192;      // uint32 [kHistCopies][2][256] after the header
 constexpr int64_t kHeaderBytes = 65536;
 static_assert(sizeof(WsHeader) <= kHistPartOff, "header");
+static_assert(offsetof(WsHeader, error) == 3084 && offsetof(WsHeader, above) == 3136,
+              "header offsets the host reads (engine.py: error word, WS_ABOVE_OFF)");
 
 __host__ __device__ inline int64_t n_tiles_of(int64_t n_px) { return (n_px + kTilePx - 1) / kTilePx; }
 __host__ __device__ inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
@@ -251,6 +258,21 @@ __device__ inline void mu1_run(int lo, int hi, const double (&ip)[4], const doub
       }
     }
   }
+}
+
+// Pixels of a 256-bin histogram at or above bin m (the wave's sum).  n when m <= 0: the clipped
+// difference histogram puts every negative white - black into bin 0, so it cannot tell which of
+// them reach a threshold below 1 (for white, m <= 0 is every pixel anyway).
+__device__ int64_t hist_at_least_wave(const uint32_t* h, int m, int64_t n) {
+  if (m <= 0) return n;
+  const int lane = threadIdx.x & 63;
+  uint64_t a = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b = 64 * j + lane;
+    if (b >= m) a += h[b];
+  }
+  return int64_t(wave_sum(a));
 }
 
 __device__ double otsu_wave(const uint32_t* h, int64_t n) {
@@ -483,6 +505,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
       const double thr = tid == 0 ? p.shadow_val : p.contrast_val;
       const int m = int_threshold(thr, tid == 0 ? 0 : -255);
       if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
+      ws->above[tid] = p.n_px;                 // manual thresholds: no histogram, no bound
     }
     return;
   }
@@ -595,9 +618,11 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   if (otsu) {
     if (wave < 2) {                            // wave 0: white, wave 1: clip(w-b); concurrently
       const double thr = (p.dbg & 16) ? 100.0 : otsu_wave(hg + 256 * wave, p.n_px);
+      const int m = int_threshold(thr, wave == 0 ? 0 : -255);
+      const int64_t above = hist_at_least_wave(hg + 256 * wave, m, p.n_px);
       if ((tid & 63) == 0) {
-        const int m = int_threshold(thr, wave == 0 ? 0 : -255);
         if (wave == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
+        ws->above[wave] = above;
       }
     }
   } else if (tid < 2) {
@@ -611,6 +636,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
     }
     const int m = int_threshold(thr, tid == 0 ? 0 : -255);
     if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
+    ws->above[tid] = p.n_px;                   // (the percentile histogram is black's: no bound)
   }
   for (int i = tid; i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
   if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
@@ -686,9 +712,11 @@ __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint
   __syncthreads();
   if (wave < 2) {                              // wave 0: white, wave 1: clip(w-b); concurrently
     const double thr = otsu_wave(hg + 256 * wave, n_px);
+    const int m = int_threshold(thr, wave == 0 ? 0 : -255);
+    const int64_t above = hist_at_least_wave(hg + 256 * wave, m, n_px);
     if ((tid & 63) == 0) {
-      const int m = int_threshold(thr, wave == 0 ? 0 : -255);
       if (wave == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
+      ws->above[wave] = above;
     }
   }
   for (int i = tid; act && i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
@@ -953,6 +981,7 @@ __device__ inline uint32_t pack_code(const MainParams& p, int c, int r) {
 struct TriOut {
   double x, y, z;      // column-stream point (row_mode 0/1), or column point (row_mode 2)
   double rx, ry, rz;   // row-stream point (row_mode 2)
+  double t, tr;        // their ray parameters: (x, y, z) = Oc + r * t, (rx, ry, rz) = Oc + r * tr
   uint32_t keep;       // bit 0 column stream, bit 1 row stream
 };
 
@@ -1089,6 +1118,8 @@ __device__ inline TriOut tri_combine(const MainParams& p, const TriPlanes& pl, d
     t = okc ? (-num) / den : 0.0;
   }
   o.x = p.o0 + r0 * t; o.y = p.o1 + r1 * t; o.z = p.o2 + r2 * t;
+  o.t = t;
+  o.tr = 0.0;
   o.keep = okc;
   o.rx = o.ry = o.rz = 0.0;
   if constexpr (ROW_MODE == 1) {                          // epipolar filter, processing.py:197-201
@@ -1107,6 +1138,7 @@ __device__ inline TriOut tri_combine(const MainParams& p, const TriPlanes& pl, d
       tr = okr ? (-nr) / dr : 0.0;
     }
     o.rx = p.o0 + r0 * tr; o.ry = p.o1 + r1 * tr; o.rz = p.o2 + r2 * tr;
+    o.tr = tr;
     o.keep |= uint32_t(okr) << 1;
   }
   return o;
@@ -1569,6 +1601,17 @@ __device__ inline void st_out(T* a, T v) {
 // goes to LDS word l (its index within the tile's kept points), and the workgroup writes the
 // tile's contiguous byte range [3 base, 3 (base + agg)) as 16-byte aligned stores, each lane
 // packing six staged words into four output dwords; the two ragged end chunks go byte by byte.
+#ifndef SLG_X64_KEEP_T
+#define SLG_X64_KEEP_T 1                   // f64 XYZ, pinhole rays: t in registers, ray recomputed in phase D
+#endif
+#ifndef SLG_X64_STAGE
+#define SLG_X64_STAGE 0                    // f64 XYZ: per-wave LDS window, 16-byte aligned stores (r5a: 405.2
+#endif                                     // vs 405.9 us alone, 376.0 vs 364.2 with KEEP_T: off)
+#ifndef SLG_X64_PAIR
+#define SLG_X64_PAIR 0                     // f64 XYZ: (x, y) as one 16-byte store at 8-byte alignment + z
+#endif
+constexpr int kX64Window = 3 * 64 + 2;     // one round of a wave: 64 points + the alignment pad
+
 #ifndef SLG_BGR_STAGE
 #define SLG_BGR_STAGE 0                    // 329.3 vs 324.5 us per 16-view launch (profiles/r4j): off
 #endif
@@ -1602,9 +1645,9 @@ __device__ inline void bgr_tile_store(uint8_t* gb, int64_t base, int agg, const 
 // Phase B of main3 for rounds [i, i + G) (item m = tid + 256 * round), FAST path: the G items'
 // loads and fp64 chains are independent, so their plane gathers are in flight together.
 // tri_rounds: i is a compile-time multiple of G (the unrolled group loop); tri_rounds_at: any i.
-template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NP = 0>
+template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NP = 0, int NC = 3>
 __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, const uint2* s_item,
-                                     XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
+                                     XT (&pts)[NS][kIt][NC], uint64_t (&km)[NS][kIt]) {
   const int tid = threadIdx.x;
   TriOut o[G];
   TriPlanes pl[G];
@@ -1634,9 +1677,14 @@ __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, co
 #pragma unroll
     for (int r = 0; r < kIt; ++r)
       if (r == i + h) {
-        pts[0][r][0] = XT(o[h].x); pts[0][r][1] = XT(o[h].y); pts[0][r][2] = XT(o[h].z);
-        if constexpr (ROW_MODE == 2) {
-          pts[NS - 1][r][0] = XT(o[h].rx); pts[NS - 1][r][1] = XT(o[h].ry); pts[NS - 1][r][2] = XT(o[h].rz);
+        if constexpr (NC == 1) {                   // the ray parameters only (x64_keep_t)
+          pts[0][r][0] = o[h].t;
+          if constexpr (ROW_MODE == 2) pts[NS - 1][r][0] = o[h].tr;
+        } else {
+          pts[0][r][0] = XT(o[h].x); pts[0][r][1] = XT(o[h].y); pts[0][r][2] = XT(o[h].z);
+          if constexpr (ROW_MODE == 2) {
+            pts[NS - 1][r][0] = XT(o[h].rx); pts[NS - 1][r][1] = XT(o[h].ry); pts[NS - 1][r][2] = XT(o[h].rz);
+          }
         }
 #pragma unroll
         for (int s = 0; s < NS; ++s) km[s][r] = __ballot((keep >> s) & 1u);
@@ -1644,10 +1692,10 @@ __device__ inline void tri_rounds_at(const MainParams& p, int i, int n_items, co
   }
 }
 
-template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NP = 0>
+template <int G, int ROW_MODE, int RAYS, typename XT, int NS, int kIt, int NP = 0, int NC = 3>
 __device__ inline void tri_rounds(const MainParams& p, int i, int n_items, const uint2* s_item,
-                                  XT (&pts)[NS][kIt][3], uint64_t (&km)[NS][kIt]) {
-  tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt, NP>(p, i, n_items, s_item, pts, km);
+                                  XT (&pts)[NS][kIt][NC], uint64_t (&km)[NS][kIt]) {
+  tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt, NP, NC>(p, i, n_items, s_item, pts, km);
 }
 
 // PROF: the profiling instance (SLG_DBG set): honours the ablation bits of MainParams::dbg and
@@ -1674,7 +1722,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // the carried batch's nibble planes and histograms in LDS of their own (68 KB per workgroup,
   // two per CU): each wave stages its lane data as soon as phase A ends, no extra barrier
   // (289.7 vs 291.6 us per launch against aliasing the item arrays after phase B)
-  __shared__ uint2 s_hstage[(kB / 64) * 256];                         // [wave][4 planes][64 lanes]
+  __shared__ __attribute__((aligned(16))) uint2 s_hstage[(kB / 64) * 256];   // [wave][4 planes][64 lanes]
+  static_assert(kX64Window * 8 <= 256 * 8, "phase D's per-wave f64 window fits the wave's staging");
   __shared__ uint32_t s_hn[512];                                      // histograms
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1805,7 +1854,12 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // Item m = tid + kB * i: every wave gets an equal share of the tile's valid pixels.
   // Points stay in registers across the look-back (recomputing them after it instead frees
   // ~15 VGPRs for a fifth wave per SIMD but measured 6% slower).
-  XT pts[NS][kIt][3];
+  // f64 XYZ with pinhole rays (x64_keep_t): only t (and tr) stay in registers across the look-back
+  // -- 48 VGPRs of points pushed the instance past 128 VGPRs into scratch -- and phase D
+  // recomputes the ray from the item's (u, v): the same code on the same inputs, the same bits.
+  constexpr bool KT = XYZ64 && RAYS == SLG_RAYS_PINHOLE && SLG_X64_KEEP_T;
+  constexpr int NC = KT ? 1 : 3;
+  XT pts[NS][kIt][NC];
   uint64_t km[NS][kIt];
   static_assert(kIt % SLG_TRI_GROUP == 0, "grouped rounds");
   const bool trivial = PROF && (p.dbg & 2);          // ablation: no triangulation arithmetic
@@ -1865,13 +1919,20 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
         uint32_t keep;
         if (trivial) {
           keep = in ? (ROW_MODE == 2 ? 3u : 1u) : 0u;
-          pts[0][i][0] = XT(code & 0xffff); pts[0][i][1] = XT(code >> 16); pts[0][i][2] = XT(u);
-          if constexpr (ROW_MODE == 2) { pts[NS - 1][i][0] = XT(v); pts[NS - 1][i][1] = 0; pts[NS - 1][i][2] = 0; }
+          if constexpr (NC == 3) {
+            pts[0][i][0] = XT(code & 0xffff); pts[0][i][1] = XT(code >> 16); pts[0][i][2] = XT(u);
+            if constexpr (ROW_MODE == 2) { pts[NS - 1][i][0] = XT(v); pts[NS - 1][i][1] = 0; pts[NS - 1][i][2] = 0; }
+          }
         } else {
           const TriOut o = tri_item<ROW_MODE, RAYS>(p, code, u, v);
           keep = in ? o.keep : 0u;
-          pts[0][i][0] = XT(o.x); pts[0][i][1] = XT(o.y); pts[0][i][2] = XT(o.z);
-          if constexpr (ROW_MODE == 2) { pts[NS - 1][i][0] = XT(o.rx); pts[NS - 1][i][1] = XT(o.ry); pts[NS - 1][i][2] = XT(o.rz); }
+          if constexpr (NC == 1) {
+            pts[0][i][0] = o.t;
+            if constexpr (ROW_MODE == 2) pts[NS - 1][i][0] = o.tr;
+          } else {
+            pts[0][i][0] = XT(o.x); pts[0][i][1] = XT(o.y); pts[0][i][2] = XT(o.z);
+            if constexpr (ROW_MODE == 2) { pts[NS - 1][i][0] = XT(o.rx); pts[NS - 1][i][1] = XT(o.ry); pts[NS - 1][i][2] = XT(o.rz); }
+          }
         }
 #pragma unroll
         for (int s = 0; s < NS; ++s) km[s][i] = __ballot((keep >> s) & 1u);
@@ -1972,6 +2033,26 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   }
   if (false)
 #endif
+  // the point of round i, stream s: from registers, or (KT) Oc + r * t with the ray recomputed
+  auto point_of = [&](int s, int i, XT& x, XT& y, XT& z) {
+    if constexpr (KT) {
+      const uint32_t uv = s_item[item_slot(tid + kB * i)].y;
+      double r0, r1, r2;
+      if (p.rays_fast) tri_ray<RAYS, true>(p, int(uv & 0xffffu), int(uv >> 16), r0, r1, r2);
+      else tri_ray<RAYS, false>(p, int(uv & 0xffffu), int(uv >> 16), r0, r1, r2);
+      const double t = pts[s][i][0];
+      x = p.o0 + r0 * t; y = p.o1 + r1 * t; z = p.o2 + r2 * t;
+    } else {
+      x = pts[s][i][0]; y = pts[s][i][NC - 1 < 1 ? 0 : 1]; z = pts[s][i][NC - 1];
+    }
+  };
+  // f64 XYZ through a per-wave LDS window (SLG_X64_STAGE, off: measured no faster): a wave's kept points of one round are
+  // one contiguous run of the cloud, written as 16-byte aligned stores -- 24 bytes per point in
+  // 1.5 stores and whole lines, where each lane's three 8-byte stores at a 24-byte stride touch
+  // 12 lines per instruction.  No workgroup barrier: the window is the wave's own (the carried
+  // histogram staging, free once phase C's barrier has passed).
+  constexpr bool XS = XYZ64 && SLG_X64_STAGE;
+  double* s_xw = reinterpret_cast<double*>(s_hstage) + wave * kX64Window;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int64_t base = int64_t(s_excl[s]);
@@ -1979,12 +2060,48 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     uint8_t* gb = s == 0 ? p.bgr : p.scratch_bgr;
 #pragma unroll
     for (int i = 0; i < kIt; ++i) {
+      if (XS && km[s][i] != 0ull && !(PROF && (p.dbg & 128))) {      // wave-uniform
+        const int64_t q0 = base + s_loc[s][i][wave];                   // the wave's first point
+        const int n = __popcll(km[s][i]);
+        // a = 1: the run starts in the middle of a 16-byte pair; window slot 0 is then a pad
+        const int a = int(((reinterpret_cast<uintptr_t>(gx) >> 3) + 3 * uint64_t(q0)) & 1u);
+        if ((km[s][i] >> lane) & 1ull) {
+          XT x, y, z;
+          point_of(s, i, x, y, z);
+          const int w = 3 * __popcll(km[s][i] & lt) + a;
+          s_xw[w] = double(x); s_xw[w + 1] = double(y); s_xw[w + 2] = double(z);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int nd = 3 * n + a;                                     // window doubles incl. the pad
+        double* g = reinterpret_cast<double*>(gx) + 3 * q0 - a;       // 16-byte aligned
+        for (int d0 = 2 * lane; d0 < nd; d0 += 128) {
+          if (d0 >= a && d0 + 1 < nd) {
+            st_out(reinterpret_cast<double2*>(g + d0), *reinterpret_cast<const double2*>(s_xw + d0));
+          } else {
+            if (d0 >= a) st_out(g + d0, s_xw[d0]);
+            if (d0 + 1 < nd) st_out(g + d0 + 1, s_xw[d0 + 1]);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");       // reads done before the next round's writes
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
       if ((km[s][i] >> lane) & 1ull) {
         const int l = s_loc[s][i][wave] + __popcll(km[s][i] & lt);
         const int64_t q = base + l;
         const uint32_t c = s_bgr[bgr_slot(tid + kB * i)];
-        if (!(PROF && (p.dbg & 128))) {              // PROF ablation bit 7: no XYZ stores
-          st_out(gx + 3 * q, pts[s][i][0]); st_out(gx + 3 * q + 1, pts[s][i][1]); st_out(gx + 3 * q + 2, pts[s][i][2]);
+        if (!XS && !(PROF && (p.dbg & 128))) {       // PROF ablation bit 7: no XYZ stores
+          XT x, y, z;
+          point_of(s, i, x, y, z);
+          if constexpr (XYZ64 && SLG_X64_PAIR) {
+            typedef double d2a8 __attribute__((ext_vector_type(2), aligned(8)));
+            *reinterpret_cast<d2a8*>(gx + 3 * q) = d2a8{double(x), double(y)};
+            st_out(gx + 3 * q + 2, z);
+          } else {
+            st_out(gx + 3 * q, x); st_out(gx + 3 * q + 1, y); st_out(gx + 3 * q + 2, z);
+          }
         }
         if (SLG_BGR_STAGE) {
           s_stage[s * kStageWords + l] = c;

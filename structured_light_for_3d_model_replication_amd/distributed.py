@@ -54,6 +54,29 @@ def batch_summary(success: int, total: int, device=None) -> tuple[int, int]:
     return int(t[0]), int(t[1])
 
 
+PER_RANK_KEYS = ("views", "points", "kernel_ms", "d2h_ms", "step_ms")
+
+
+def per_rank_table(row: dict, device=None) -> list[dict]:
+    """Every rank's timing row on every rank (one all_gather of a float64 vector; identity
+    without a process group): ``row`` holds :data:`PER_RANK_KEYS` (numbers), the result is the
+    rows in rank order with ``rank`` added.  A bench line reports them beside its max-over-ranks
+    headline, so a slow rank (its kernels, or its PCIe copies) is visible."""
+    vec = torch.tensor([float(row[k]) for k in PER_RANK_KEYS], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized():
+        parts = [torch.empty_like(vec) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, vec)
+    else:
+        parts = [vec]
+    out = []
+    for r, v in enumerate(parts):
+        d = {"rank": r}
+        for k, x in zip(PER_RANK_KEYS, v.tolist()):
+            d[k] = int(x) if k in ("views", "points") else round(x, 4)
+        out.append(d)
+    return out
+
+
 def gather_clouds(xyz: torch.Tensor, bgr: torch.Tensor, dst: int = 0):
     """Exact-size gatherv of variable-size clouds to ``dst`` over torch.distributed (gloo or
     RCCL): the counts go by one all_gather, then every rank sends exactly its own points

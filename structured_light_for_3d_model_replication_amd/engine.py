@@ -358,6 +358,7 @@ class Reconstructor:
 
 
 MAX_VIEWS_PER_LAUNCH = 16     # kMaxViews in csrc/slgpu.hip
+WS_ABOVE_OFF = 3136           # offsetof(WsHeader, above) in csrc/slgpu.hip (static_assert there)
 
 
 @dataclass
@@ -450,6 +451,30 @@ class BatchReconstructor:
     def stats(self, pb: PreparedBatch, stream=None):
         N.check(N.lib().slg_decode_stats_batch(pb.caps, pb.n, ctypes.byref(pb.dp), self._ws(pb.slot),
                                                self.ws_stride, _stream(stream)))
+
+    def valid_bounds(self, frames, cfg: DecodeConfig, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        """Upper bounds of each capture's valid pixels -- so of its row_mode 0/1 points -- from
+        one batched stats pass over white / black (slot 0; Otsu: min(#white >= smin,
+        #(white - black) >= cmin) from the histograms the thresholds come from, the header's
+        ``above`` words; other modes: H*W).  ``out``: int64 device tensor [len(frames)], filled
+        stream-ordered in groups of ``max_views`` (no host sync)."""
+        n = len(frames)
+        out = torch.empty(n, dtype=torch.int64, device=self.device) if out is None else out
+        words = self.workspace.view(torch.int64)
+        dp = cfg.struct()
+        with torch.cuda.stream(stream or torch.cuda.current_stream(self.device)):
+            for g in range(0, n, self.max_views):
+                grp = frames[g: g + self.max_views]
+                for f in grp:
+                    if (f.height, f.width) != (self.height, self.width):
+                        raise ValueError(f"engine built for {self.width}x{self.height}, got {f.width}x{f.height}")
+                caps = (N.Capture * len(grp))(*[f.capture() for f in grp])
+                N.check(N.lib().slg_decode_stats_batch(caps, len(grp), ctypes.byref(dp), self._ws(0),
+                                                       self.ws_stride, _stream(stream)))
+                base = torch.arange(len(grp), device=self.device) * (self.ws_stride // 8) + WS_ABOVE_OFF // 8
+                above = words[torch.stack([base, base + 1], 1)]            # [k, 2]
+                out[g: g + len(grp)] = above.min(1).values
+        return out
 
     def main(self, pb: PreparedBatch, events=None, stream=None):
         N.check(N.lib().slg_decode_triangulate_batch(pb.caps, pb.n, ctypes.byref(pb.dp),

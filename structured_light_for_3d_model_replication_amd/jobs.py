@@ -14,11 +14,21 @@ MI355X's HBM.  :class:`ResidentJob` runs such a job with every view already resi
   view j starts at the sum of the capacity hints of views < j.  The arena ends with ``H*W``
   points of slack, so from any view's start there are at least ``H*W`` points to the arena's end
   -- the C ABI's capacity contract (``slg_cloud.capacity >= H*W``) holds for every view and no
-  store can leave the allocation.  A view whose count exceeds its hint has written into its
-  successors' regions: :meth:`ResidentJob.overflowed` names such views, and
-  :meth:`ResidentJob.damaged` adds the views whose region an overflow reached (re-run all of
-  them into clouds of their own).  With exact hints (a previous pass over the same frames, or per-view valid-pixel
-  counts) 576 4K clouds take 41 GB instead of the 72 GB of worst-case slots.
+  store can leave the allocation.
+
+**Sizing.**  By default the job sizes itself on the device (:func:`device_capacity_hints`): one
+batched stats pass over every view's white and black frames gives each view's Otsu histograms,
+and ``min(#white >= smin, #(white - black) >= cmin)`` -- read off the same histograms the
+thresholds come from -- bounds its valid pixels, hence its row_mode 0/1 points.  The pass reads
+2 of a view's 46 frames; no earlier pass over the job is needed.  Hints given by the caller (an
+earlier pass's counts, say) are taken as they are.
+
+**Isolation.**  A view whose count exceeds its hint has written into its successors' regions:
+:meth:`ResidentJob.overflowed` names such views and :meth:`ResidentJob.damaged` adds the views
+whose region an overflow reached.  :meth:`ResidentJob.recover` re-runs all of them into clouds of
+their own, and :meth:`ResidentJob.cloud` refuses a damaged view that was not recovered -- the
+reference isolates each folder in the same spirit (``server/processing.py:323-330``: one
+folder's failure is logged and the loop goes on with the next).
 """
 from __future__ import annotations
 
@@ -67,11 +77,31 @@ def stage_copies(sources, plan, device=None):
     return out
 
 
+def device_capacity_hints(views, cfg: E.DecodeConfig, engine: E.BatchReconstructor | None = None,
+                          stream=None) -> list[int]:
+    """Per-view upper bounds of the row_mode 0/1 point count, computed on the device
+    (``BatchReconstructor.valid_bounds``: one batched stats pass over white / black, the bound
+    read off the Otsu histograms).  One host sync at the end."""
+    if not views:
+        return []
+    h, w = views[0].height, views[0].width
+    eng = engine or E.BatchReconstructor(h, w, min(E.MAX_VIEWS_PER_LAUNCH, len(views)),
+                                         device=views[0].data.device, slots=1)
+    return [int(x) for x in eng.valid_bounds(views, cfg, stream=stream).tolist()]
+
+
+class DamagedViewError(RuntimeError):
+    """A resident job's view whose cloud another view's overflow may have overwritten."""
+
+
 class ResidentJob:
-    """One job over HBM-resident views of one geometry (see the module docstring)."""
+    """One job over HBM-resident views of one geometry (see the module docstring).
+
+    ``capacity_hints``: ``"device"`` (default: :func:`device_capacity_hints`), a list of ints (one
+    per view, taken as given), or ``None`` (H*W per view: the worst case)."""
 
     def __init__(self, views, cfg: E.DecodeConfig, calib: E.DeviceCalib, batch: int = 4, row_mode: int = 1,
-                 epipolar_tol: float = 2.0, xyz_f64: bool = False, capacity_hints=None, device=None):
+                 epipolar_tol: float = 2.0, xyz_f64: bool = False, capacity_hints="device", device=None):
         if not views:
             raise ValueError("a job needs at least one view")
         if cfg.thresh_mode != "otsu" or cfg.variant != "processing":
@@ -83,21 +113,39 @@ class ResidentJob:
         self.height, self.width, self.n_px = h, w, h * w
         self.device = device or self.views[0].data.device
         self.batch = max(1, min(int(batch), E.MAX_VIEWS_PER_LAUNCH))
-        hints = capacity_hints if capacity_hints is not None else [self.n_px] * len(self.views)
+        self.cfg, self.calib, self.row_mode, self.tol, self.xyz_f64 = cfg, calib, row_mode, epipolar_tol, xyz_f64
+        self.engine = E.BatchReconstructor(h, w, self.batch, device=self.device, slots=4)
+        if isinstance(capacity_hints, str):
+            if capacity_hints != "device":
+                raise ValueError("capacity_hints: 'device', a list of ints, or None")
+            hints = device_capacity_hints(self.views, cfg, self.engine)
+            self.hints_source = "device"
+        elif capacity_hints is None:
+            hints, self.hints_source = [self.n_px] * len(self.views), "worst_case"
+        else:
+            hints, self.hints_source = capacity_hints, "caller"
         if len(hints) != len(self.views):
             raise ValueError("one capacity hint per view")
         self.hints = [int(x) for x in hints]
         self.clouds, self.offsets, self.xyz, self.bgr, self.counts = packed_clouds(
             self.n_px, self.hints, xyz_f64, self.device)
-        self.engine = E.BatchReconstructor(h, w, self.batch, device=self.device, slots=4)
         groups = [list(range(g, min(g + self.batch, len(self.views)))) for g in range(0, len(self.views), self.batch)]
         self.groups = groups
         self.batches = [self.engine.prepare([self.views[k] for k in g], cfg, calib, [self.clouds[k] for k in g],
                                             row_mode, epipolar_tol, slot=i % 4) for i, g in enumerate(groups)]
+        self._recovered: dict = {}            # view -> (xyz, bgr) of its own, or the exception of its re-run
+        self._rec = None
+
+    @property
+    def arena_points(self) -> int:
+        """Points the packed arena holds (the hints plus H*W of slack)."""
+        return int(self.xyz.shape[0])
 
     def run(self, s0, s1):
         """Enqueue the whole job (first four groups' stats passes, then one fused launch per group
-        on the two streams); afterwards ``s0`` has joined ``s1``.  No host sync."""
+        on the two streams); afterwards ``s0`` has joined ``s1``.  No host sync.  Forgets any
+        earlier :meth:`recover`."""
+        self._recovered.clear()
         s1.wait_stream(s0)
         self.engine.run_pipelined(self.batches, s0, s1, mode="fused2")
         s0.wait_stream(s1)
@@ -121,7 +169,36 @@ class ResidentJob:
             bad.update(k for k in range(j + 1, len(self.hints)) if self.offsets[k] < end)
         return sorted(bad)
 
+    def recover(self, counts=None, stream=None) -> list[int]:
+        """Re-run every damaged view (:meth:`damaged`) alone into a cloud of its own (worst-case
+        capacity), stream-ordered after the job.  A view whose re-run raises keeps the exception,
+        which :meth:`cloud` raises for it.  Returns the views re-run."""
+        counts = self.host_counts() if counts is None else counts
+        bad = [j for j in self.damaged(counts) if j not in self._recovered]
+        if bad and self._rec is None:
+            self._rec = E.Reconstructor(self.height, self.width, device=self.device)
+        for j in bad:
+            try:
+                c = self._rec.reconstruct(self.views[j], self.cfg, self.calib, self.row_mode, self.tol,
+                                          xyz_f64=self.xyz_f64, stream=stream)
+                self._recovered[j] = c.result()
+            except Exception as e:  # noqa: BLE001 - per-view isolation
+                self._recovered[j] = e
+        return bad
+
     def cloud(self, j, counts=None):
-        """``(xyz, bgr)`` of view j (device slices of the arena)."""
-        n = (self.host_counts() if counts is None else counts)[j]
+        """``(xyz, bgr)`` of view j: its recovered cloud after :meth:`recover`, else the arena
+        slices.  Raises :class:`DamagedViewError` for a damaged view that was not recovered (its
+        points may belong to another view), and the re-run's exception for one whose re-run
+        failed."""
+        r = self._recovered.get(j)
+        if isinstance(r, Exception):
+            raise r
+        if r is not None:
+            return r
+        counts = self.host_counts() if counts is None else counts
+        if j in self.damaged(counts):
+            raise DamagedViewError(f"view {j}: its cloud overflowed its capacity hint or was overwritten by "
+                                   "an earlier view's overflow; call recover() first")
+        n = counts[j]
         return self.xyz[self.offsets[j]: self.offsets[j] + n], self.bgr[self.offsets[j]: self.offsets[j] + n]

@@ -7,6 +7,9 @@ write an ASCII PLY.  Here the same work is a pipeline whose stages overlap:
 * **read** (thread pool, up to ``depth`` folders ahead): discover the files, decode the frames the
   decode needs straight into a **pinned** host frame stack (native 8-bit gray PNG decoder into the
   stack rows; colour frames into a pinned RGB(A) stack, converted on the device);
+* **device decode** (decode stream, issued first): the last folders of a batch of PNG captures
+  (:func:`device_share`) are read as zlib streams only and inflated by ONE GPU launch while the
+  host threads decode the others -- the two decoders' rates add;
 * **upload** (copy stream): async H2D of a group of up to ``group`` views;
 * **reconstruct** (compute stream): device texture (frame 0 replicated, or frame 0's BGR from the
   colour upload), then ONE batched stats launch + ONE fused decode/triangulate launch for the
@@ -15,8 +18,8 @@ write an ASCII PLY.  Here the same work is a pipeline whose stages overlap:
 * **collect**: counts; each view's PLY body formatted on the device (``slg_ply_format``, on a
   stream of its own beside the next group's kernels) and copied into pinned host memory as
   bytes (a cloud with a value the device formatter leaves to the host: its float64 points);
-* **write** (writer thread): header + body (byte-identical ASCII PLY; ``slg_ply_write`` for
-  host clouds).
+* **write** (``writers`` threads, files in parallel): header + body (byte-identical ASCII PLY;
+  ``slg_ply_write`` for host clouds).
 
 Per-folder behaviour is the reference's: folders without images are skipped with its message,
 an exception in any stage of one folder is logged as ``❌ Error in <folder>: <msg>`` and the loop
@@ -29,6 +32,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 
@@ -90,14 +94,42 @@ def _decode_rgb(path) -> np.ndarray:
     return a
 
 
+def device_png_mode() -> str:
+    """Which PNG captures the GPU decodes (``slg_png_decode_device``), from SLG_PNG_DEVICE:
+    ``"1"`` all of them, ``"0"`` none, unset or ``"auto"`` a share of a batch (the last folders,
+    :func:`device_share`) while host threads decode the rest.  SLG_PNG_PIL forces the host."""
+    if os.environ.get("SLG_PNG_PIL"):
+        return "off"
+    v = os.environ.get("SLG_PNG_DEVICE", "auto")
+    return "all" if v == "1" else "off" if v == "0" else "auto"
+
+
 def device_png_enabled() -> bool:
-    """PNG captures decoded on the GPU (``slg_png_decode_device``) with SLG_PNG_DEVICE=1; off by
-    default.  The inflate is one wave per stream, ~225 ms per 1080p frame, so it needs 16 views
-    per launch (704 streams) to reach 13.8 ms per view against 20 ms for the host decoder on the
-    box's 16 CPUs, and in this pipeline the host decoder gives the lower s/view (DESIGN §4,
-    profiles/r4n, r4o).  Correct and tested (tests/test_png_device.py), kept for hosts with
-    fewer CPUs per GPU."""
-    return os.environ.get("SLG_PNG_DEVICE", "0") == "1" and not os.environ.get("SLG_PNG_PIL")
+    """Whether a lone capture read (:func:`read_view` without ``device_png``) goes to the device
+    decoder: only with SLG_PNG_DEVICE=1.  The inflate is one wave per stream, ~225 ms per 1080p
+    frame whatever the launch size (profiles/r4n), so one view alone is far faster on
+    the host threads."""
+    return device_png_mode() == "all"
+
+
+# Host PNG decode on the box's 16 CPUs: ~20 ms per C2 view (profiles/r4o); one device inflate
+# launch: ~225 ms whatever its size, up to 768 streams in flight (17 views of 44 frames).  A batch
+# overlaps the two when the host has about that long of its own work: the last n - 12 folders
+# (at most 16) go to ONE device launch started at the beginning, the host threads decode the
+# rest meanwhile.
+HOST_AHEAD = 12
+DEVICE_MAX_VIEWS = 16
+
+
+def device_share(n_folders: int, mode: str | None = None) -> int:
+    """Folders (the last ones of the batch) whose PNG frames the GPU decodes."""
+    mode = device_png_mode() if mode is None else mode
+    if mode == "off":
+        return 0
+    if mode == "all":
+        return n_folders
+    ahead = int(os.environ.get("SLG_PNG_HOST_AHEAD", HOST_AHEAD))
+    return max(0, min(DEVICE_MAX_VIEWS, n_folders - ahead))
 
 
 def read_view_z(folder: str, files, need, pool: PinnedPool) -> HostView | None:
@@ -118,8 +150,12 @@ def read_view_z(folder: str, files, need, pool: PinnedPool) -> HostView | None:
 
     def one(k):
         return L.slg_png_zstream(os.fsencode(files[need[k]]), ctypes.c_void_p(base + offs[k]), caps[k], infos[k])
-    with ThreadPoolExecutor(max_workers=min(FR.decode_threads(), len(need))) as ex:
-        rcs = list(ex.map(one, range(len(need))))
+    try:
+        with ThreadPoolExecutor(max_workers=min(FR.decode_threads(), len(need))) as ex:
+            rcs = list(ex.map(one, range(len(need))))
+    except BaseException:
+        pool.put(buf)                   # (a file vanished, an executor error): the buffer goes back
+        raise
     shapes = {tuple(i[:3]) for i in infos}
     if any(rcs) or len(shapes) != 1 or next(iter(shapes))[2] not in (1, 3, 4):
         pool.put(buf)
@@ -217,12 +253,14 @@ def upload_views(hvs, stream) -> list:
     ``slg_png_decode_device`` launch over all their frames (a view's 44 streams alone leave the
     GPU nearly idle: the decode is one wave per stream).  The host buffers must stay alive until
     ``stream`` reaches here.  Returns the DeviceFrames in order."""
-    # gray captures whose texture is frame 0 (the 8-bit gray PNGs the reference's scanner writes)
-    # run in GRAY texture mode: no texture buffer, the kernels take the colour from frame 0
-    devs = [E.DeviceFrames.allocate(hv.n_files, hv.height, hv.width, gray=_gray_mode(hv)) for hv in hvs]
     sp = ctypes.c_void_p(stream.cuda_stream)
     L = N.lib()
     with torch.cuda.stream(stream):
+        # allocated on `stream` (its pool in the caching allocator): if a later step raises, the
+        # buffers freed here can only be handed out again behind the work already queued on it
+        # gray captures whose texture is frame 0 (the 8-bit gray PNGs the reference's scanner
+        # writes) run in GRAY texture mode: no texture buffer, the kernels take frame 0's bytes
+        devs = [E.DeviceFrames.allocate(hv.n_files, hv.height, hv.width, gray=_gray_mode(hv)) for hv in hvs]
         pngs = [(hv, dev) for hv, dev in zip(hvs, devs) if hv.kind == "png_z"]
         if pngs:
             decode_png_device(pngs, stream)
@@ -331,41 +369,118 @@ class _Group:
     event: object = None
     batch: object = None
     clouds: list = field(default_factory=list)
+    uploaded: object = None         # device-decoded group: the event its uploads + inflate end on
+    gpu_events: tuple = None        # (start, end) around its reconstruct launches
+
+
+class PipelineStats:
+    """Busy time per stage of one :meth:`BatchPipeline.run` (seconds; summed over threads for
+    the host stages, HIP events for the GPU ones) and the split between the decoders."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self.read_s = 0.0             # host: file read + decode (or zstream read) into pinned memory
+        self.write_s = 0.0            # host: PLY files written
+        self.device_decode_ms = 0.0   # GPU: H2D of the zlib streams + inflate + un-filter
+        self.gpu_ms = 0.0             # GPU: reconstruct launches (stats + fused) of every group
+        self.folders_host = 0
+        self.folders_device = 0
+        self.wall_s = 0.0
+
+    def add(self, key: str, v: float):
+        with self._lock:
+            setattr(self, key, getattr(self, key) + v)
+
+    def as_dict(self) -> dict:
+        return {"wall_s": round(self.wall_s, 4), "read_busy_s": round(self.read_s, 4),
+                "write_busy_s": round(self.write_s, 4), "device_decode_ms": round(self.device_decode_ms, 3),
+                "gpu_reconstruct_ms": round(self.gpu_ms, 3), "folders_host_decoded": self.folders_host,
+                "folders_device_decoded": self.folders_device}
+
+
+LAST_STATS: PipelineStats | None = None     # the stats of the last BatchPipeline.run (tools/e2e_files.py)
 
 
 class BatchPipeline:
-    """The pipeline of this module's docstring for one decode configuration + calibration."""
+    """The pipeline of this module's docstring for one decode configuration + calibration.
+
+    PNG decode is split between the host threads and the GPU (:func:`device_share`): the last
+    folders of the batch are read as zlib streams and decoded by ONE device launch issued at the
+    start, on a stream of its own, while the host threads decode the others; the device group is
+    reconstructed when the pipeline reaches it, in folder order.  PLY files are written by
+    ``writers`` threads (a C2 view's ASCII PLY is ~60 MB)."""
 
     def __init__(self, cfg: E.DecodeConfig, calib: dict, row_mode=1, epipolar_tol=2.0, group: int = 8,
-                 depth: int | None = None, log=print, order=("bmp", "png"), device_ply: bool = True):
+                 depth: int | None = None, log=print, order=("bmp", "png"), device_ply: bool = True,
+                 writers: int = 4, device_views: int | None = None):
         if row_mode not in (0, 1, 2):
             raise ValueError("row_mode must be 0, 1 or 2")
         self.cfg, self.calib, self.row_mode, self.tol = cfg, calib, int(row_mode), float(epipolar_tol)
         self.group = max(1, min(int(group), E.MAX_VIEWS_PER_LAUNCH))
-        self.depth = depth or 2 * self.group
+        self.depth = depth or max(2 * self.group, 16)
         self.log, self.order = log, order
+        self.writers = max(1, int(writers))
+        self.device_views = device_views          # None: device_share() of the batch
         self.pool = PinnedPool()
         self.copy_stream = torch.cuda.Stream()
         self.compute_stream = torch.cuda.Stream()
         self.format_stream = torch.cuda.Stream()     # PLY bodies of group k beside group k+1's kernels
+        self.decode_stream = torch.cuda.Stream()     # the device-decoded group's H2D + inflate
         self.formatter = PLY.DeviceFormatter()
         self.device_ply = device_ply
         self.engines: dict = {}
         self.tables: dict = {}
         self._slot = 0
+        self._max_views = self.group
+        self.stats = PipelineStats()
 
     def _engine(self, h, w):
         key = (h, w)
         if key not in self.engines:
-            beng = E.BatchReconstructor(h, w, self.group, slots=2)
-            clouds = [[E.Cloud(h * w, self.row_mode, True) for _ in range(self.group)] for _ in range(2)]
+            n = self._max_views
+            beng = E.BatchReconstructor(h, w, n, slots=2)
+            clouds = [[E.Cloud(h * w, self.row_mode, True) for _ in range(n)] for _ in range(2)]
             self.engines[key] = (beng, clouds)
             self.tables[key] = E.DeviceCalib(self.calib, h, w)
         return self.engines[key], self.tables[key]
 
+    def _read(self, folder, device_png: bool) -> HostView:
+        t = time.perf_counter()
+        try:
+            hv = read_view(folder, self.cfg, self.pool, self.order, device_png=device_png)
+        finally:
+            self.stats.add("read_s", time.perf_counter() - t)
+        self.stats.add("folders_device" if hv.kind == "png_z" else "folders_host", 1)
+        return hv
+
     # ---- stages
-    def _launch(self, g: _Group):
-        """Upload g's views (copy stream) and launch their reconstruction (compute stream)."""
+    def _upload(self, g: _Group, got, stream):
+        """g.views += the uploads of ``got`` [(entry index, HostView)] on ``stream``: one upload
+        (one PNG decode launch) for all of them, or -- when that raises -- view by view, with the
+        device decoder's views read again for the host decoder, so a failure stays with its
+        folder."""
+        try:
+            devs = upload_views([hv for _, hv in got], stream) if got else []
+            g.views += [(k, hv, d) for (k, hv), d in zip(got, devs)]
+        except Exception:  # noqa: BLE001
+            # what the failed attempt queued (H2D from the pinned stacks, decode launches) must
+            # finish before those stacks are reused or re-read
+            stream.synchronize()
+            for k, hv in got:
+                try:
+                    if hv.kind == "png_z":             # the device decoder's views: the host decodes them
+                        hv2 = self._read(hv.folder, device_png=False)
+                        for t in hv.pinned:
+                            self.pool.put(t)
+                        hv = hv2
+                    g.views.append((k, hv, upload_view(hv, self.copy_stream)))
+                except Exception as e:  # noqa: BLE001
+                    g.errors[k] = e
+                    for t in hv.pinned:
+                        self.pool.put(t)
+
+    @staticmethod
+    def _results(g: _Group):
         got = []
         for k, (folder, fut) in enumerate(g.entries):
             if fut is None:
@@ -374,23 +489,36 @@ class BatchPipeline:
                 got.append((k, fut.result()))
             except Exception as e:  # noqa: BLE001 - per-folder isolation like the reference
                 g.errors[k] = e
-        try:                                           # one upload (one PNG decode launch) per group
-            devs = upload_views([hv for _, hv in got], self.copy_stream) if got else []
-            g.views += [(k, hv, d) for (k, hv), d in zip(got, devs)]
-        except Exception:  # noqa: BLE001 - then view by view, so the failure stays with its folder
-            for k, hv in got:
-                try:
-                    g.views.append((k, hv, upload_view(hv, self.copy_stream)))
-                except Exception as e:  # noqa: BLE001
-                    g.errors[k] = e
+        return got
+
+    def _start_device_group(self, g: _Group):
+        """Upload + inflate the device group's zlib streams now, on the decode stream."""
+        got = self._results(g)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(self.decode_stream)
+        self._upload(g, got, self.decode_stream)
+        ev1.record(self.decode_stream)
+        g.uploaded = (ev0, ev1)
+
+    def _launch(self, g: _Group):
+        """Upload g's views (copy stream; done already for the device group) and launch their
+        reconstruction (compute stream)."""
+        if g.uploaded is None:
+            self._upload(g, self._results(g), self.copy_stream)
         if not g.views:
             return
-        ev = torch.cuda.Event()
-        ev.record(self.copy_stream)
-        self.compute_stream.wait_event(ev)
+        if g.uploaded is not None:
+            self.compute_stream.wait_event(g.uploaded[1])
+            self.compute_stream.wait_stream(self.copy_stream)     # (a fallback's per-view uploads)
+        else:
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+            self.compute_stream.wait_event(ev)
         shapes = {(d.height, d.width) for _, _, d in g.views}
         slot = self._slot
         self._slot ^= 1
+        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        g0.record(self.compute_stream)
         try:
             if len(shapes) != 1:
                 raise ValueError("views of different sizes")
@@ -401,6 +529,8 @@ class BatchPipeline:
             g.clouds = outs
         except Exception:  # noqa: BLE001 - the group falls back to one view at a time
             g.batch = None
+        g1.record(self.compute_stream)
+        g.gpu_events = (g0, g1)
         g.event = torch.cuda.Event()
         g.event.record(self.compute_stream)
 
@@ -410,12 +540,15 @@ class BatchPipeline:
         if not g.views:
             return res
         g.event.synchronize()
+        self.stats.add("gpu_ms", g.gpu_events[0].elapsed_time(g.gpu_events[1]))
+        if g.uploaded is not None:
+            self.stats.add("device_decode_ms", g.uploaded[0].elapsed_time(g.uploaded[1]))
         from .processing import reconstruct_view
         redo = {k for k, _, dev in g.views if png_failed(dev)}
         for k, hv, dev in g.views:               # a frame the device decoder refused: the host decodes
             if k in redo:                        # the whole view again (general path) and runs it alone
                 try:
-                    hv2 = read_view(hv.folder, self.cfg, self.pool, self.order, device_png=False)
+                    hv2 = self._read(hv.folder, device_png=False)
                     try:
                         dev2 = upload_view(hv2, self.copy_stream)
                         self.copy_stream.synchronize()
@@ -454,24 +587,50 @@ class BatchPipeline:
 
     def run(self, subfolders, write) -> int:
         """Process ``subfolders`` in order; ``write(folder, (P, C)) -> output name``."""
+        global LAST_STATS
         from .processing import has_images
-        log = self.log
+        t_run = time.perf_counter()
+        self.stats = LAST_STATS = PipelineStats()
         entries = [(f, has_images(f)) for f in subfolders]
         success = 0
-        with ThreadPoolExecutor(max_workers=2) as reader, ThreadPoolExecutor(max_workers=1) as writer:
+        order = [f for f, ok in entries if ok]
+        mode = device_png_mode()
+        n_dev = device_share(len(order), mode) if self.device_views is None else max(0, min(int(self.device_views), len(order)))
+        if mode == "all" and self.device_views is None:
+            n_dev = 0                               # every group is read for the device decoder
+        if n_dev:
+            self._max_views = max(self.group, n_dev)
+        dev_first = len(order) - n_dev              # the device group: the last n_dev image folders
+        cut = len(entries)
+        if n_dev:
+            cut = next(i for i, (f, ok) in enumerate(entries) if ok and f == order[dev_first])
+
+        def timed_write(folder, result):
+            t = time.perf_counter()
+            try:
+                return write(folder, result)
+            finally:
+                self.stats.add("write_s", time.perf_counter() - t)
+
+        with ThreadPoolExecutor(max_workers=2) as reader, ThreadPoolExecutor(max_workers=self.writers) as writer:
             futs = {}
-            order = [f for f, ok in entries if ok]
+            all_dev = mode == "all"
+            dev_group = None
+            if n_dev:                                # the device group's zlib streams first: its
+                ents = entries[cut:]                 # launch starts while the host decodes the rest
+                dev_group = _Group([(f, reader.submit(self._read, f, True) if ok else None) for f, ok in ents])
+            host_order = order[:dev_first]
             nxt = 0
 
             def prefetch(upto):
                 nonlocal nxt
-                while nxt < len(order) and nxt < upto:
-                    futs[order[nxt]] = reader.submit(read_view, order[nxt], self.cfg, self.pool, self.order)
+                while nxt < len(host_order) and nxt < upto:
+                    futs[host_order[nxt]] = reader.submit(self._read, host_order[nxt], all_dev)
                     nxt += 1
 
-            # groups: consecutive entries holding up to `group` folders with images
+            # host groups: consecutive entries holding up to `group` folders with images
             groups, cur, n_img = [], [], 0
-            for f, ok in entries:
+            for f, ok in entries[:cut]:
                 cur.append((f, ok))
                 n_img += ok
                 if n_img == self.group:
@@ -479,20 +638,29 @@ class BatchPipeline:
                     cur, n_img = [], 0
             if cur:
                 groups.append(cur)
-            done_imgs = 0
             prefetch(self.depth)
+            if dev_group is not None:
+                self._start_device_group(dev_group)
+            done_imgs = 0
             prev = None
-            for gi, ents in enumerate(groups + [None]):
+            todo = list(groups)                    # host groups as entry lists (made when reached)
+            if dev_group is not None:
+                todo.append(dev_group)
+            for gi, item in enumerate(todo + [None]):
                 g = None
-                if ents is not None:
-                    g = _Group([(f, futs.pop(f) if ok else None) for f, ok in ents])
+                if isinstance(item, _Group):
+                    g = item
+                elif item is not None:
+                    g = _Group([(f, futs.pop(f) if ok else None) for f, ok in item])
+                if g is not None:
                     self._launch(g)
                 if prev is not None:
                     res = self._collect(prev)
                     done_imgs += sum(1 for _, fut in prev.entries if fut is not None)
                     prefetch(done_imgs + self.depth)
-                    success += self._report(prev, res, write, writer)
+                    success += self._report(prev, res, timed_write, writer)
                 prev = g
+        self.stats.wall_s = time.perf_counter() - t_run
         return success
 
     def _report(self, g: _Group, res, write, writer) -> int:

@@ -88,6 +88,12 @@ def _body(rank, tmp, q):
                 f.write(str(rank))
 
         D.process_batch_sharded("unused.mat", tmp, log_callback=logs.append, process_source=proc)
+        # the per-rank timing rows bench.py --config c3 reports beside its headline
+        rows = D.per_rank_table({"views": 18, "points": 1000 + rank, "kernel_ms": 0.5 + rank,
+                                 "d2h_ms": 2.25 * (rank + 1), "step_ms": 3.0 + rank})
+        assert [r["rank"] for r in rows] == [0, 1]
+        assert [r["points"] for r in rows] == [1000, 1001] and [r["d2h_ms"] for r in rows] == [2.25, 4.5]
+        assert [r["kernel_ms"] for r in rows] == [0.5, 1.5] and all(r["views"] == 18 for r in rows)
         q.put((rank, logs))
 
 

@@ -251,3 +251,47 @@ def test_c5_resident_job(mods):
     torch.cuda.synchronize()
     assert job2.overflowed() == [2]
     assert job2.damaged() == [2, 3]                     # view 3's region begins inside view 2's overflow
+    # refusal: a damaged view's arena slice is never handed out
+    for j in (2, 3):
+        with pytest.raises(J.DamagedViewError):
+            job2.cloud(j)
+    # recovery: the damaged views re-run into clouds of their own, equal to the oracle's
+    assert job2.recover() == [2, 3]
+    for j in range(4):
+        x, b = job2.cloud(j)
+        assert np.array_equal(b.cpu().numpy(), want[plan[j]][1]), j
+        _xyz32_close(x.cpu().numpy(), want[plan[j]][0])
+    # self-sizing: the default hints come from the device (Otsu histograms of white / black), an
+    # upper bound of every view's count -- no earlier pass over the job, nothing overflows
+    job3 = J.ResidentJob(views, cfg, dcal, batch=2)
+    assert job3.hints_source == "device"
+    assert all(h >= n for h, n in zip(job3.hints, hints)), (job3.hints, hints)
+    assert sum(job3.hints) < len(views) * H * W         # tighter than the worst case
+    job3.run(s0, s1)
+    torch.cuda.synchronize()
+    counts3 = job3.host_counts()
+    assert counts3 == hints and job3.damaged(counts3) == []
+    for j, p in enumerate(plan):
+        x, b = job3.cloud(j, counts3)
+        assert np.array_equal(b.cpu().numpy(), want[p][1]), j
+        _xyz32_close(x.cpu().numpy(), want[p][0])
+
+
+def test_valid_bounds_match_histogram_counts(mods, scan):
+    """``BatchReconstructor.valid_bounds`` (the resident jobs' device sizing): per view
+    min(#(white > ts), #((white - black) > tc)) with the Otsu thresholds of
+    server/processing.py:63-72, exactly; >= the valid pixels; 20 views in groups of 16 + 4."""
+    E, N = mods
+    cal, views = scan
+    vs = views[:20]
+    cfg = E.DecodeConfig(1920, 1080, 11, 11, "otsu")
+    eng = E.BatchReconstructor(1080, 1920, 16, slots=1)
+    got = eng.valid_bounds([E.DeviceFrames(list(v.frames), v.texture) for v in vs], cfg).tolist()
+    for v, g in zip(vs, got):
+        w = v.frames[0].astype(np.float32)
+        b = v.frames[1].astype(np.float32)
+        ts = O.otsu_threshold(w.astype(np.uint8))
+        tc = O.otsu_threshold(np.clip(w - b, 0, 255).astype(np.uint8))
+        want = min(int(np.count_nonzero(w > ts)), int(np.count_nonzero((w - b) > tc)))
+        assert g == want
+        assert g >= int(np.count_nonzero(O.mask_processing(v.frames[0], v.frames[1])))

@@ -5,7 +5,7 @@ give round 2-3's 12-view one-stream shape), one subprocess per variant, rounds i
 The time is the step period: one HIP event pair around the timed launches, both streams joined
 (median_us = us per launch = per step).
 
-    python tools/ab.py --libs build_ab/base.so,build_ab/w5b6.so [--rounds 3] [--launches 200]
+    python tools/ab.py --libs build_ab/base.so,build_ab/w5b6.so [--rounds 3] [--launches 200] [--xyz f64]
 
 Each worker loads the same cached rendered views (rendered once into /tmp), runs warmup + timed
 launches with HIP events on the launch stream, and checks every view's point count and the
@@ -50,7 +50,7 @@ def worker(a):
     dcal = E.DeviceCalib(cal, H, W, device=dev, tables=a.tables != "none", keep_table=a.tables == "rays")
     cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
     beng = E.BatchReconstructor(H, W, B, device=dev, slots=NSL)
-    clouds = [[E.Cloud(H * W, 1, False, device=dev) for _ in range(B)] for _ in range(NSL)]
+    clouds = [[E.Cloud(H * W, 1, a.xyz == "f64", device=dev) for _ in range(B)] for _ in range(NSL)]
     preps = {}
 
     def prep(b):
@@ -81,6 +81,10 @@ def worker(a):
     cl = clouds[last % NSL]
     counts = [int(c.count.item()) for c in cl]
     chk = float(sum(c.xyz[: int(c.count.item())].double().sum().item() for c in cl))
+    # and the bits: a wrapping int64 sum of the XYZ words and the colours
+    bits = sum(int(c.xyz[: int(c.count.item())].reshape(-1).view(torch.int32).to(torch.int64).sum().item())
+               + int(c.bgr[: int(c.count.item())].to(torch.int64).sum().item()) for c in cl)
+    chk = f"{chk!r}/{bits}"
     err = int(np.frombuffer(beng.header(0, 0)[3084:3088].cpu().numpy().tobytes(), np.uint32)[0])
     print(json.dumps({"lib": os.environ.get("SLG_LIB", "default"), "median_us": round(statistics.median(us), 2),
                       "p10_us": round(us[len(us) // 10], 2), "p90_us": round(us[9 * len(us) // 10], 2),
@@ -96,6 +100,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16, help="views per fused launch (bench: 16)")
     ap.add_argument("--pipeline", default="fused2", help="fused2 (bench: two streams) | fused (one stream)")
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--xyz", default="f32", help="f32 | f64 (the drop-in's float64 clouds)")
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--tables", default="num", help="worker: num | none (DeviceCalib numerator tables) | rays (also the Nc ray table)")
     ap.add_argument("--variants", default="", help="comma list of lib[:tables] (overrides --libs)")
@@ -117,7 +122,7 @@ def main():
             if path:
                 env["SLG_LIB"] = path
             cmd = [sys.executable, __file__, "--worker", "--launches", str(a.launches), "--warmup", str(a.warmup),
-                   "--batch", str(a.batch), "--pipeline", a.pipeline]
+                   "--batch", str(a.batch), "--pipeline", a.pipeline, "--xyz", a.xyz]
             if opt:
                 cmd += ["--tables", opt]
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout)

@@ -1,12 +1,20 @@
 #!/usr/bin/env python
 """End-to-end file path of the drop-in: ``process_multi_ply(mode='batch')`` over C2 view folders
-of 8-bit PNG captures (PNG decode on a host thread pool with the next folder prefetched, H2D,
-fused kernels, native ASCII PLY writer).  Reported in DESIGN.md, never the bench metric.
+of 8-bit PNG captures, the reference GUI's live path (``server/gui.py:1360-1376`` ->
+``server/processing.py:314-334``; the C3 folder layout of ``server/gui.py:1718,1753``).
+Reported in DESIGN.md, never the bench metric.
 
-Prints one JSON line: seconds per view for the whole batch with the PNGs decoded on the GPU
-(``slg_png_decode_device``: host reads files only) and on host threads, and the serial cost of
-the parts (frame read [+ host decode], H2D [+ device decode] + kernels + D2H, PLY write) measured
-view by view; and whether both decoders gave the same PLY bytes.
+Prints one JSON line: seconds per view for the whole batch under each decoder split
+
+* ``host``   -- every folder's PNGs decoded on host threads (``SLG_PNG_DEVICE=0``);
+* ``auto``   -- the product default: the last folders' zlib streams inflated by one GPU launch
+  while the host threads decode the rest (``pipeline.device_share``);
+* ``device`` -- every folder on the GPU decoder (``SLG_PNG_DEVICE=1``),
+
+at the given views-per-launch groups (``SLG_BATCH_VIEWS``), each run's per-stage busy times
+(``pipeline.LAST_STATS``: host read/decode and PLY write busy seconds summed over threads, GPU
+device-decode and reconstruct milliseconds from HIP events), and whether every run wrote the same
+PLY bytes.  ``--parts`` adds the serial cost of the stages measured view by view.
 """
 from __future__ import annotations
 
@@ -16,6 +24,7 @@ import os
 import sys
 import tempfile
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -23,11 +32,16 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--views", type=int, default=16)
-    ap.add_argument("--groups", type=int, nargs="+", default=[1, 4, 16])
+    ap.add_argument("--views", type=int, default=36)
+    ap.add_argument("--runs", default="host:1,host:4,host:8,auto:4,auto:8,device:16",
+                    help="comma list of decoder:group (decoder host | auto | device)")
+    ap.add_argument("--reps", type=int, default=1, help="repetitions of the whole list (interleaved)")
+    ap.add_argument("--parts", action="store_true", help="also the serial per-stage costs")
+    ap.add_argument("--out", default="", help="also write the JSON here")
     args = ap.parse_args()
 
     from structured_light_for_3d_model_replication_amd import calibration, synth
+    from structured_light_for_3d_model_replication_amd import pipeline as PL
     from structured_light_for_3d_model_replication_amd import processing as PR
 
     rig = synth.default_rig(1920, 1080, 1920, 1080)
@@ -35,52 +49,82 @@ def main():
         calib = os.path.join(tmp, "calib.mat")
         calibration.save_mat(calib, rig.tables())
         root = os.path.join(tmp, "scan")
-        for i in range(args.views):
+        t = time.perf_counter()
+
+        def make(i):
             v = synth.render_view(rig, 360.0 * i / args.views, seed=i, n_present=44)
             synth.write_capture(v, os.path.join(root, f"obj_{i:02d}_scan"))
-        folders = sorted(os.path.join(root, d) for d in os.listdir(root))
+        with ThreadPoolExecutor(8) as ex:
+            list(ex.map(make, range(args.views)))
+        print(f"[e2e] wrote {args.views} captures in {time.perf_counter() - t:.1f}s", file=sys.stderr, flush=True)
+        folders = [f.path for f in os.scandir(root) if f.is_dir()]     # the order batch mode uses
         kw = dict(n_sets_col=11, n_sets_row=10)
         PR.ProcessingLogic.process_multi_ply(calib, folders[0], "single", log_callback=lambda m: None, **kw)  # warm-up
-        batch_s, plys = {}, {}
-        for dec in ("device", "host"):                # PNG inflate + un-filter on the GPU, or host threads
-            os.environ["SLG_PNG_DEVICE"] = "1" if dec == "device" else "0"
-            for g in args.groups:                     # views per batched launch (SLG_BATCH_VIEWS)
-                os.environ["SLG_BATCH_VIEWS"] = str(g)
+        runs = [r.split(":") for r in args.runs.split(",") if r]
+        res, plys = {}, {}
+        env = {"host": "0", "auto": "auto", "device": "1"}
+        for rep in range(args.reps):
+            for dec, g in runs:
+                os.environ["SLG_PNG_DEVICE"] = env[dec]
+                os.environ["SLG_BATCH_VIEWS"] = g
                 t0 = time.perf_counter()
                 PR.ProcessingLogic.process_multi_ply(calib, root, "batch", log_callback=lambda m: None, **kw)
-                batch_s[f"{dec}_png_group{g}"] = round((time.perf_counter() - t0) / args.views, 4)
-            plys[dec] = [open(os.path.join(f, os.path.basename(f) + ".ply"), "rb").read() for f in folders]
+                dt = time.perf_counter() - t0
+                key = f"{dec}_group{g}"
+                st = PL.LAST_STATS.as_dict()
+                res.setdefault(key, []).append({"s_per_view": round(dt / args.views, 4), **st})
+                print(f"[e2e] rep {rep} {key}: {dt / args.views:.4f} s/view {st}", file=sys.stderr, flush=True)
+                plys[key] = [open(os.path.join(f, os.path.basename(f) + ".ply"), "rb").read() for f in folders]
+        first = next(iter(plys.values()))
+        out = {"what": "process_multi_ply batch over C2 PNG folders (end to end), s/view per decoder split",
+               "views": args.views, "runs": res,
+               "best": min(((k, min(x["s_per_view"] for x in v)) for k, v in res.items()), key=lambda kv: kv[1]),
+               "ply_bytes_equal_all_runs": all(p == first for p in plys.values()),
+               "ply_mb_per_view": round(sum(len(b) for b in first) / len(first) / 1e6, 2),
+               "decode_threads": PR.FR.decode_threads(), "host_cpus": os.cpu_count(),
+               "cpu_quota": _quota()}
 
-        # the pipeline's stages one view at a time, serially (what the overlap hides)
-        import torch
-        from structured_light_for_3d_model_replication_amd import pipeline as PL
-        cfg = PR.E.DecodeConfig(1920, 1080, 11, 10, "otsu")
-        cal = calibration.load_mat(calib)
-        pool = PL.PinnedPool()
-        s = torch.cuda.Stream()
-        parts = {}
-        pts = 0
-        for dec in ("device", "host"):
-            t_read = t_rec = t_ply = 0.0
-            for f in folders:
-                t = time.perf_counter(); hv = PL.read_view(f, cfg, pool, device_png=dec == "device"); t_read += time.perf_counter() - t
-                t = time.perf_counter()
-                dev = PL.upload_view(hv, s)
-                s.synchronize()
-                P, C = PR.reconstruct_view(dev, cfg, cal, 1, 2.0)
-                t_rec += time.perf_counter() - t
-                for b in hv.pinned:
-                    pool.put(b)
-                t = time.perf_counter(); PR.ProcessingLogic._save_ply(P, C, os.path.join(tmp, "x.ply")); t_ply += time.perf_counter() - t
-                pts += len(P)
-            n = len(folders)
-            parts[dec] = {"read_pinned": round(t_read / n, 4), "h2d_decode_kernels_d2h": round(t_rec / n, 4),
-                          "ply_write": round(t_ply / n, 4)}
-        print(json.dumps({"what": "process_multi_ply batch, C2 PNG folders (end to end)", "views": n,
-                          "points_per_view": pts // (2 * n), "s_per_view_batch": batch_s,
-                          "s_per_view_parts_serial": parts,
-                          "ply_bytes_device_equal_host": plys["device"] == plys["host"],
-                          "decode_threads": PR.FR.decode_threads(), "host_cpus": os.cpu_count()}), flush=True)
+        if args.parts:                                 # the stages one view at a time, serially
+            import torch
+            cfg = PR.E.DecodeConfig(1920, 1080, 11, 10, "otsu")
+            cal = calibration.load_mat(calib)
+            pool = PL.PinnedPool()
+            s = torch.cuda.Stream()
+            parts = {}
+            for dec in ("device", "host"):
+                t_read = t_rec = t_ply = 0.0
+                for f in folders[:16]:
+                    t = time.perf_counter()
+                    hv = PL.read_view(f, cfg, pool, device_png=dec == "device")
+                    t_read += time.perf_counter() - t
+                    t = time.perf_counter()
+                    dev = PL.upload_view(hv, s)
+                    s.synchronize()
+                    P, C = PR.reconstruct_view(dev, cfg, cal, 1, 2.0)
+                    t_rec += time.perf_counter() - t
+                    for b in hv.pinned:
+                        pool.put(b)
+                    t = time.perf_counter()
+                    PR.ProcessingLogic._save_ply(P, C, os.path.join(tmp, "x.ply"))
+                    t_ply += time.perf_counter() - t
+                n = len(folders[:16])
+                parts[dec] = {"read_pinned": round(t_read / n, 4), "h2d_decode_kernels_d2h": round(t_rec / n, 4),
+                              "ply_write": round(t_ply / n, 4)}
+            out["s_per_view_parts_serial"] = parts
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+
+
+def _quota():
+    try:
+        sys.path.insert(0, ROOT)
+        import bench
+        return bench.cpu_quota()
+    except Exception:  # noqa: BLE001
+        return None
 
 
 if __name__ == "__main__":

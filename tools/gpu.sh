@@ -17,7 +17,7 @@
 #   prof             kernel trace + FETCH/WRITE PMC passes (tools/gpu_profile.sh) -> <tag>/prof/
 #   prof=<name>=<args>   the same for bench.py <args> (commas -> spaces)  -> <tag>/prof_<name>/
 #   sq               SQ counter passes (tools/pmc_main.sh)              -> <tag>/sq/
-#   ab=<libA>,<libB>[,...][,rounds]  interleaved A/B of library builds (tools/ab.py) -> ab.log
+#   ab=<libA>,<libB>[,...][,rounds]  interleaved A/B of library builds (tools/ab.py; AB_ARGS) -> ab_<n>.log
 #   py=<script>=<args>   python <script> <args> (commas -> spaces)      -> py_<n>.log
 #   kt=<script>=<args>   the same under rocprofv3 --kernel-trace --stats  -> kt_<n>/ (+ kt_<n>.log)
 #   mem              device memory as torch sees it                     -> mem.log
@@ -65,9 +65,10 @@ for step in "$@"; do
     ab)
       libs=${rest%,[0-9]*}; rounds=${rest##*,}
       [ "$libs" = "$rest" ] && rounds=4
-      timeout -k 10 900 python tools/ab.py --libs "$libs" --rounds "$rounds" > "$O/ab.log" 2>&1 \
-        || { echo "[gpu.sh] AB FAILED"; tail -20 "$O/ab.log"; exit $n; }
-      tail -3 "$O/ab.log" ;;
+      # AB_ARGS: extra tools/ab.py arguments for every ab step (e.g. "--xyz f64")
+      timeout -k 10 900 python tools/ab.py --libs "$libs" --rounds "$rounds" $AB_ARGS > "$O/ab_$n.log" 2>&1 \
+        || { echo "[gpu.sh] AB FAILED"; tail -20 "$O/ab_$n.log"; exit $n; }
+      tail -3 "$O/ab_$n.log" ;;
     py)
       script=${rest%%=*}; args=${rest#*=}
       [ "$args" = "$rest" ] && args=""

@@ -36,6 +36,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 import numpy as np  # noqa: E402
 
 WORKLOADS = {
+    # c1: _gray_decode(files, n_cols=1024, n_rows=1080) with the default n_sets, row frames absent,
+    # row_mode 0 (bench.py's c1)
+    "c1": dict(cam=(1280, 720), proj=(1024, 1080), nsets=(11, 11), n_present=22, row_mode=0),
     "c2": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 10), n_present=44),
     "c3": dict(cam=(1920, 1080), proj=(1920, 1080), nsets=(11, 11), n_present=None),
     "c4": dict(cam=(6000, 4000), proj=(3840, 2160), nsets=(12, 12), n_present=None),
@@ -65,6 +68,7 @@ def main():
     for name in args.configs.split(","):
         wl = WORKLOADS[name]
         (W, H), (PW, PH), (nc, nr) = wl["cam"], wl["proj"], wl["nsets"]
+        rm = wl.get("row_mode", 1)
         rig = synth.default_rig(W, H, PW, PH)
         cal = rig.tables()
         cal["Nc"] = np.asfortranarray(cal["Nc"])
@@ -79,16 +83,16 @@ def main():
 
             def ref():
                 c, r, m, tex = PL._gray_decode(paths, n_cols=PW, n_rows=PH, n_sets_col=nc, n_sets_row=nr)
-                return PL._reconstruct_point_cloud(c, r, m, tex, cal, row_mode=1, epipolar_tol=2.0)
+                return PL._reconstruct_point_cloud(c, r, m, tex, cal, row_mode=rm, epipolar_tol=2.0)
 
             def port():
                 c, r, m, tex = R.gray_decode(frames, view.texture, n_cols=PW, n_rows=PH, n_sets_col=nc,
                                              n_sets_row=nr)
-                return R.reconstruct(c, r, m, tex, cal, row_mode=1, epipolar_tol=2.0)
+                return R.reconstruct(c, r, m, tex, cal, row_mode=rm, epipolar_tol=2.0)
 
             def oracle():
                 c, r, m = O.decode_processing(frames, n_cols=PW, n_rows=PH, n_sets_col=nc, n_sets_row=nr)
-                return O.reconstruct_processing(c, r, m, view.texture, cal, row_mode=1)
+                return O.reconstruct_processing(c, r, m, view.texture, cal, row_mode=rm)
 
             want = None
             for rep in range(args.reps):
@@ -106,7 +110,7 @@ def main():
         med = {k: statistics.median(v) for k, v in times.items()}
         pts = float(np.mean(points))
         result["configs"][name] = {
-            "camera": f"{W}x{H}", "projector": f"{PW}x{PH}", "bits": f"{nc}+{nr}", "row_mode": 1,
+            "camera": f"{W}x{H}", "projector": f"{PW}x{PH}", "bits": f"{nc}+{nr}", "row_mode": rm,
             "views": args.views, "points_per_view": int(pts),
             "median_s": {k: round(v, 4) for k, v in med.items()},
             "mpts_per_s": {k: round(pts / v / 1e6, 3) for k, v in med.items()},

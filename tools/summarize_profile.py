@@ -33,11 +33,13 @@ def rows_of(path, kernel):
         return [r for r in csv.DictReader(f) if kernel in r["Kernel_Name"]]
 
 
-TILES_PER_VIEW = {"c2": 507, "c4": 5860, "c5": 2025}     # ceil(H*W / 4096): 1920x1080, 6000x4000, 3840x2160
+TILES_PER_VIEW = {"c1": 225, "c2": 507, "c4": 5860, "c5": 2025}   # ceil(H*W / 4096): 1280x720, 1920x1080, 6000x4000, 3840x2160
 
 
-def pmc_file(config: str) -> str:
-    return "pmc_main_kernel.json" if config == "c2" else f"pmc_main_kernel_{config}.json"
+def pmc_file(config: str, xyz: str = "f32") -> str:
+    """bench.py's name for the config's committed PMC summary (pmc_main_kernel[_<config>][_f64].json)."""
+    key = config if xyz == "f32" else ("f64" if config == "c2" else f"{config}_f64")
+    return "pmc_main_kernel.json" if key == "c2" else f"pmc_main_kernel_{key}.json"
 
 
 def main():
@@ -48,6 +50,7 @@ def main():
                     help="bench config profiled: sets --tiles-per-view and which profiles/pmc_main_kernel*.json "
                          "is refreshed (c2: pmc_main_kernel.json, else pmc_main_kernel_<config>.json)")
     ap.add_argument("--tiles-per-view", type=int, default=0, help="default: ceil(H*W / 4096) of --config")
+    ap.add_argument("--xyz", choices=["f32", "f64"], default="f32", help="the profiled bench's --xyz (f64: *_f64.json)")
     ap.add_argument("--timed-last", type=int, default=0,
                     help="also report the mean over the last N launches of the most frequent grid (the "
                          "bench's timed steps: the trace run's --steps; settle/warmup launches excluded)")
@@ -123,8 +126,8 @@ def main():
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     if per and not a.no_refresh:
-        with open(os.path.join(ROOT, "profiles", pmc_file(a.config)), "w") as f:
-            json.dump({"tag": a.tag, "config": a.config, "kernel": a.kernel, "hbm_bytes_per_view": out["hbm_bytes_per_view"],
+        with open(os.path.join(ROOT, "profiles", pmc_file(a.config, a.xyz)), "w") as f:
+            json.dump({"tag": a.tag, "config": a.config, "xyz": a.xyz, "kernel": a.kernel, "hbm_bytes_per_view": out["hbm_bytes_per_view"],
                        "fetch_bytes_per_view": round(per["FETCH_SIZE"]) if "FETCH_SIZE" in per else None,
                        "write_bytes_per_view": out.get("write_size_bytes_per_view"),
                        "formula": out["units"]}, f, indent=1)
