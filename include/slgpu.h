@@ -308,6 +308,13 @@ typedef struct slg_png_frame {
 int32_t slg_png_zstream(const char *path, uint8_t *buf, int64_t cap, int32_t *info /* [4] */);
 int64_t slg_png_raw_bytes(int32_t width, int32_t height, int32_t channels);
 int32_t slg_png_decode_device(const slg_png_frame *frames, int32_t n, int32_t *status, void *stream);
+/* A stream for the device PNG decode that leaves CUs free (hipExtStreamCreateWithCUMask): every
+ * `reserve_every`-th CU of the current device is left out of its mask, so a long inflate launch
+ * (one 50 KB-LDS wave per stream, ~225 ms) cannot occupy every CU and the batch pipeline's fused
+ * launches of host-decoded views keep running beside it.  *stream = the hipStream_t; returns 0
+ * or SLG_ERR_*.  slg_stream_destroy releases it. */
+int32_t slg_stream_create_reserving(int32_t reserve_every, void **stream);
+int32_t slg_stream_destroy(void *stream);
 
 /* ---- Multi-GPU: the final point-cloud gather of a view-sharded scan.
  * Replaces nothing in the reference (its batch loop is serial, server/processing.py:314-334);

@@ -116,6 +116,8 @@ EXPORTS = {
     "slg_png_zstream": (c_i32, [ctypes.c_char_p, c_vp, c_i64, ctypes.POINTER(c_i32)]),
     "slg_png_raw_bytes": (c_i64, [c_i32, c_i32, c_i32]),
     "slg_png_decode_device": (c_i32, [c_vp, c_i32, c_vp, c_vp]),
+    "slg_stream_create_reserving": (c_i32, [c_i32, c_vp]),
+    "slg_stream_destroy": (c_i32, [c_vp]),
     "slg_rays_match_pinhole": (c_i32, [c_vp, c_i32, c_i32, c_dbl, c_dbl, c_dbl, c_dbl, c_vp, c_vp]),
     "slg_rgb_to_gray": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp]),
     "slg_gray_texture": (c_i32, [c_vp, c_i64, c_vp, c_vp]),

@@ -37,6 +37,10 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
         os.replace(OUT + ".tmp", OUT)
+        if verbose:
+            print(f"built {OUT} for gfx950")
+    elif verbose:
+        print(f"{OUT} is newer than its sources ({', '.join(os.path.basename(p) for p in SRCS)}): not rebuilt")
     return OUT
 
 

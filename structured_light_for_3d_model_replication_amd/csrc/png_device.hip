@@ -19,6 +19,7 @@
 //   bytes and checks it against the stream's trailer.
 // A frame that fails any check gets a non-zero status and is decoded on the host by the caller.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include "../../include/slgpu.h"
@@ -628,3 +629,24 @@ int32_t slg_png_decode_device(const slg_png_frame* frames, int32_t n, int32_t* s
 }
 
 }  // extern "C"
+
+extern "C" int32_t slg_stream_create_reserving(int32_t reserve_every, void** stream) {
+  if (!stream || reserve_every < 2) return SLG_ERR_INVALID;
+  int dev = 0, n_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1)
+    return SLG_ERR_HIP;
+  const int n_words = (n_cu + 31) / 32;
+  uint32_t mask[64] = {};
+  if (n_words > 64) return SLG_ERR_UNSUPPORTED;
+  for (int cu = 0; cu < n_cu; ++cu)
+    if (cu % reserve_every != reserve_every - 1) mask[cu / 32] |= 1u << (cu % 32);
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, uint32_t(n_words), mask) != hipSuccess) return SLG_ERR_HIP;
+  *stream = s;
+  return SLG_OK;
+}
+
+extern "C" int32_t slg_stream_destroy(void* stream) {
+  return hipStreamDestroy(static_cast<hipStream_t>(stream)) == hipSuccess ? SLG_OK : SLG_ERR_HIP;
+}

@@ -263,7 +263,7 @@ __device__ inline void mu1_run(int lo, int hi, const double (&ip)[4], const doub
 // Pixels of a 256-bin histogram at or above bin m (the wave's sum).  n when m <= 0: the clipped
 // difference histogram puts every negative white - black into bin 0, so it cannot tell which of
 // them reach a threshold below 1 (for white, m <= 0 is every pixel anyway).
-__device__ int64_t hist_at_least_wave(const uint32_t* h, int m, int64_t n) {
+__device__ __attribute__((always_inline)) inline int64_t hist_at_least_wave(const uint32_t* h, int m, int64_t n) {
   if (m <= 0) return n;
   const int lane = threadIdx.x & 63;
   uint64_t a = 0;
@@ -275,10 +275,81 @@ __device__ int64_t hist_at_least_wave(const uint32_t* h, int m, int64_t n) {
   return int64_t(wave_sum(a));
 }
 
-__device__ double otsu_wave(const uint32_t* h, int64_t n) {
+// The two serial chains of otsu_wave run on wave-uniform registers fed from LDS: every lane
+// computes the same chain, its per-bin operands read as broadcast LDS words a chunk ahead, and
+// lane 0 stores the per-bin results back.  A step is then the chain's own fp64 ops and nothing
+// else (the readlane variant paid two v_readlane, their SGPR hazard and two v_cndmask per bin).
+// lds: kOtsuLds doubles of this wave's own.
+#ifndef SLG_OTSU_MARK
+#define SLG_OTSU_MARK(k)                   // tools/otsu_probe.hip: a timestamp per part of otsu_wave
+#endif
+#ifndef SLG_OTSU_LDS
+#define SLG_OTSU_LDS 1                     // the chains fed from LDS (0: the round-4 readlane chains)
+#endif
+constexpr int kOtsuLds = 7 * 256 + 128;   // 7 arrays of 256 bins + the chains' dump words
+constexpr int kOtsuChunk = 8;
+
+// q1[i] = q1[i-1] + p[i] in bin order (OpenCV's sequential sum), p and q1 in LDS.  Every lane
+// stores every step -- lane 0 to sq[i], the others to a dump word of their own -- so the loop
+// has no per-bin branch (an `if (lane == 0)` store cost two taken branches per bin).
+__device__ __attribute__((always_inline)) inline void q1_chain_lds(const double* sp, double* sq, double* dump) {
+  const int lane = threadIdx.x & 63;
+  double q1 = 0.0;
+#pragma unroll 1
+  for (int i0 = 0; i0 < 256; i0 += kOtsuChunk) {
+    double pp[kOtsuChunk];
+#pragma unroll
+    for (int k = 0; k < kOtsuChunk; ++k) pp[k] = sp[i0 + k];
+#pragma unroll
+    for (int k = 0; k < kOtsuChunk; ++k) {
+      q1 = q1 + pp[k];
+      *(lane == 0 ? sq + i0 + k : dump + lane) = q1;
+    }
+  }
+}
+
+// mu1_run<true> on LDS operands: over bins [lo, hi], a = mu1 * q1[i-1] + ip[i] (mu1 = 0 at lo,
+// where q1[lo-1] is taken as 0 as mu1_run does), mu1 = fma(a, y[i], a * c[i]) with
+// c[i] = fma(-q1[i], y[i], 1) * y[i] precomputed; every bin's a and mu1 stored for the check
+// (branch-free, as q1_chain_lds).
+__device__ __attribute__((always_inline)) inline void mu1_chain_lds(int lo, int hi, const double* sq, const double* sip,
+                                                                    const double* sy, const double* sc, double* sa,
+                                                                    double* sm, double* dump) {
+  const int lane = threadIdx.x & 63;
+  constexpr int C = 4;
+  double mu1 = 0.0;
+#pragma unroll 1
+  for (int i0 = lo; i0 <= hi; i0 += C) {
+    double qp[C], ipk[C], yk[C], ck[C];
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      const int i = i0 + k <= hi ? i0 + k : hi;        // (past hi: computed, never stored)
+      qp[k] = i > lo ? sq[i - 1] : 0.0;
+      ipk[k] = sip[i]; yk[k] = sy[i]; ck[k] = sc[i];
+    }
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      const double a = mu1 * qp[k] + ipk[k];
+      mu1 = fma(a, yk[k], a * ck[k]);
+      const bool mine = lane == 0 && i0 + k <= hi;
+      *(mine ? sa + i0 + k : dump + lane) = a;
+      *(mine ? sm + i0 + k : dump + 64 + lane) = mu1;
+    }
+  }
+}
+
+__device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t* h, int64_t n, double* lds) {
+  SLG_OTSU_MARK(0);
   const int lane = threadIdx.x & 63;
   const double scale = 1.0 / double(n);
   const double eps = double(__FLT_EPSILON__);
+  double* sp = lds;                 // p_i
+  double* sq = lds + 256;           // q1_i
+  double* sip = lds + 512;          // i * p_i
+  double* sy = lds + 768;           // RN(1 / q1_i) of unskipped bins
+  double* sc = lds + 1024;          // fma(-q1_i, y_i, 1) * y_i
+  double* sa = lds + 1280;          // the mu1 chain's numerators
+  double* sm = lds + 1536;          // and its mu1 values
   double pv[4], ip[4], q1r[4], yr[4], m1r[4], ar[4];
   uint64_t isum = 0;
 #pragma unroll
@@ -288,10 +359,25 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
     ip[j] = double(i) * pv[j];
     isum += uint64_t(i) * h[i];
     q1r[j] = yr[j] = m1r[j] = ar[j] = 0.0;
+    sp[i] = pv[j];
+    sip[i] = ip[j];
   }
   isum = wave_sum(isum);
   const double mu = double(isum) * scale;
-  double q1 = 0.0;                                   // 1. the q1 chain (OpenCV's order)
+  SLG_OTSU_MARK(1);
+  // 1. the q1 chain (OpenCV's order): LDS in, LDS out (wave-local: the wave's own LDS ops are
+  // in order, the fence only keeps the compiler from moving them)
+#if SLG_OTSU_LDS
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  q1_chain_lds(sp, sq, lds + 7 * 256);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int j = 0; j < 4; ++j) q1r[j] = sq[4 * lane + j];
+#else
+  double q1 = 0.0;                                   // (the readlane chain, for A/B)
   for (int l = 0; l < 64; ++l) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -300,6 +386,8 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
       q1 = nq;
     }
   }
+#endif
+  SLG_OTSU_MARK(2);
   uint32_t okr = 0;                                  // 2. bit j: bin 4*lane+j not skipped
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -308,6 +396,8 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
       okr |= 1u << j;
       yr[j] = 1.0 / q1r[j];
     }
+    sy[4 * lane + j] = yr[j];
+    sc[4 * lane + j] = fma(-q1r[j], yr[j], 1.0) * yr[j];
   }
   // 3. the mu1 chain.  The unskipped bins form one run [lo, hi]: q1 never decreases and
   // q2 = RN(1 - q1) never increases, so each skip test holds on a prefix plus a suffix of the
@@ -316,6 +406,7 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
   // numerator suits div_rn: a is 0, or at least ~1/n (an empty bin's mu1 *= q1 then / q1 moves
   // a by ulps), so n <= 2^52 keeps a far inside its range.  Anything else (never seen) takes the
   // general loop: per-bin skip flags, IEEE division when refused.
+  SLG_OTSU_MARK(3);
   const uint64_t lanes_ok = __ballot(okr != 0);
   int lo = 256, hi = -1, n_ok = 0;
   if (lanes_ok) {
@@ -326,8 +417,25 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) n_ok += __popcll(__ballot((okr >> j) & 1u));
   double mu1 = 0.0;
+  SLG_OTSU_MARK(4);
   if (n_ok == hi - lo + 1 && n <= (int64_t(1) << 52)) {
+#if SLG_OTSU_LDS
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    mu1_chain_lds(lo, hi, sq, sip, sy, sc, sa, sm, lds + 7 * 256);   // = mu1_run<true>(lo, hi, ...)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * lane + j;
+      if (i >= lo && i <= hi) { m1r[j] = sm[i]; ar[j] = sa[i]; }
+    }
+#else
     mu1_run<true>(lo, hi, ip, q1r, yr, m1r, ar);
+#endif
+    SLG_OTSU_MARK(5);
     uint32_t miss = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -353,6 +461,7 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
       }
     }
   }
+  SLG_OTSU_MARK(6);
   double best = 0.0;
   int best_i = INT_MAX;
 #pragma unroll
@@ -369,6 +478,7 @@ __device__ double otsu_wave(const uint32_t* h, int64_t n) {
     const int oi = __shfl_xor(best_i, o);
     if (ob > best || (ob == best && oi < best_i)) { best = ob; best_i = oi; }
   }
+  SLG_OTSU_MARK(7);
   return best_i == INT_MAX ? 0.0 : double(best_i);
 }
 
@@ -381,7 +491,7 @@ __device__ inline int int_threshold(double thr, int lo) {
 }
 
 // k-th smallest value (0-based) from a 256-bin histogram.
-__device__ int kth_from_hist(const uint32_t* h, int64_t k) {
+__device__ __attribute__((always_inline)) inline int kth_from_hist(const uint32_t* h, int64_t k) {
   int64_t c = 0;
   for (int v = 0; v < 256; ++v) {
     c += h[v];
@@ -391,7 +501,7 @@ __device__ int kth_from_hist(const uint32_t* h, int64_t k) {
 }
 
 // np.percentile(float32 image, 95) with method 'linear' (numpy 2.x _quantile/_lerp, float32).
-__device__ float percentile95_from_hist(const uint32_t* h, int64_t n) {
+__device__ __attribute__((always_inline)) inline float percentile95_from_hist(const uint32_t* h, int64_t n) {
   const float q = 95.0f / 100.0f;                       // np.true_divide(95, float32(100))
   const float vi = float(n - 1) * q;                    // (n-1) * quantiles, float32
   float prev = floorf(vi);
@@ -482,7 +592,8 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   // 16 sub-histograms per kind (wave x lane&3), rows padded to 257 words so the copies of one
   // bin sit in different banks: a flat background costs at most 16-way same-address adds.
   constexpr int kRow = 257;
-  __shared__ uint32_t sh[16 * 2 * kRow];
+  __shared__ __attribute__((aligned(16))) uint32_t sh[16 * 2 * kRow];
+  static_assert(512 * 4 + 2 * kOtsuLds * 8 <= 16 * 2 * kRow * 4, "Otsu tail: histograms + two waves' LDS");
   __shared__ uint4 s_stage[(kBlock / 64) * 256];   // Otsu: per wave hi/lo nibble planes of w, d
   __shared__ uint32_t s_maxd;
   __shared__ uint32_t s_last;
@@ -617,7 +728,8 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   __syncthreads();
   if (otsu) {
     if (wave < 2) {                            // wave 0: white, wave 1: clip(w-b); concurrently
-      const double thr = (p.dbg & 16) ? 100.0 : otsu_wave(hg + 256 * wave, p.n_px);
+      const double thr = (p.dbg & 16) ? 100.0
+                         : otsu_wave(hg + 256 * wave, p.n_px, reinterpret_cast<double*>(sh + 512) + wave * kOtsuLds);
       const int m = int_threshold(thr, wave == 0 ? 0 : -255);
       const int64_t above = hist_at_least_wave(hg + 256 * wave, m, p.n_px);
       if ((tid & 63) == 0) {
@@ -656,7 +768,8 @@ constexpr int kPartsBlocksMax = 64;         // workgroups per view (each sums a 
 // the view's histogram copies, takes a ticket; the last arriver runs Otsu, writes the mask
 // thresholds and resets the histogram state.  Also zeroes the view's look-back words (arming
 // the main launch that will use these thresholds; ordered by the kernel boundary).  256 lanes;
-// hg: 512 words of LDS, s_last: one.  Used by parts_kernel and by main3's finishing workgroups.
+// hg: 512 words of LDS + 2 x kOtsuLds doubles (16-byte aligned), s_last: one.  Used by
+// parts_kernel and by main3's finishing workgroups.
 __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint32_t* pp, WsHeader* ws, int64_t n_parts, int64_t n_px,
                                 int64_t n_state_words, int64_t pad_zero, int block, int n_blocks,
                                 uint32_t* hg, uint32_t* s_last) {
@@ -711,7 +824,7 @@ __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint
   }
   __syncthreads();
   if (wave < 2) {                              // wave 0: white, wave 1: clip(w-b); concurrently
-    const double thr = otsu_wave(hg + 256 * wave, n_px);
+    const double thr = otsu_wave(hg + 256 * wave, n_px, reinterpret_cast<double*>(hg + 512) + wave * kOtsuLds);
     const int m = int_threshold(thr, wave == 0 ? 0 : -255);
     const int64_t above = hist_at_least_wave(hg + 256 * wave, m, n_px);
     if ((tid & 63) == 0) {
@@ -724,7 +837,7 @@ __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint
 }
 
 __global__ __launch_bounds__(kBlock) void parts_kernel(StatsParams p) {
-  __shared__ uint32_t hg[512];
+  __shared__ __attribute__((aligned(16))) uint32_t hg[512 + 4 * kOtsuLds];   // + the Otsu tail's LDS
   __shared__ uint32_t s_last;
   otsu_from_parts(p.parts[blockIdx.y], p.wsv[blockIdx.y], p.n_parts, p.n_px, p.n_state_words, p.pad_zero,
                   int(blockIdx.x), int(gridDim.x), hg, &s_last);
@@ -1733,6 +1846,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     const int fv = int(blockIdx.x) / P.fin_blocks;
     otsu_from_parts(P.fin[fv].parts, P.fin[fv].ws, tiles, P.c.n_px, P.n_state_words, P.pad_zero,
                     int(blockIdx.x) - fv * P.fin_blocks, P.fin_blocks, reinterpret_cast<uint32_t*>(s_item), s_bgr);
+    static_assert(512 * 4 + 2 * kOtsuLds * 8 <= sizeof(s_item), "the finishing workgroups' Otsu LDS");
     return;
   }
   const int bid = int(blockIdx.x) - n_fin_wg;
@@ -2433,10 +2547,12 @@ using Main3Fn = void (*)(Main3Params);
 // pinhole rays (tools/kbench.py).
 // Decode plans main3 has specialised instances for (PLAN = (col_pairs << 4) | row_pairs), with
 // row_mode 1 or 2 and pinhole rays: C2's 11 + 10 bits (1920x1080 projector, row_scale 2), the
-// reference's default 11 + 11 (processing.py:29-30; C3, C5) and C4's 12 + 12.
+// reference's default 11 + 11 (processing.py:29-30; C3, C5) and C4's 12 + 12; row_mode 0: C1's
+// 10 column bits.
 #define SLG_PLAN_C2 0xBA
 #define SLG_PLAN_1080P 0xBB
 #define SLG_PLAN_C4 0xCC
+#define SLG_PLAN_C1 0xA0           // row_mode 0, 10 column bits (1024-wide projector), no row pairs
 
 template <int SRC>
 Main3Fn pick_main(int row_mode, int x64, int rays, int plan = 0) {
@@ -2453,6 +2569,10 @@ Main3Fn pick_main(int row_mode, int x64, int rays, int plan = 0) {
     SLG_PCASE(1, 0, SLG_PLAN_C2 | kPlanGray) SLG_PCASE(1, 1, SLG_PLAN_C2 | kPlanGray)
     SLG_PCASE(1, 0, SLG_PLAN_1080P | kPlanGray) SLG_PCASE(1, 1, SLG_PLAN_1080P | kPlanGray)
     SLG_PCASE(1, 0, SLG_PLAN_C4 | kPlanGray) SLG_PCASE(1, 1, SLG_PLAN_C4 | kPlanGray)
+  }
+  if (SRC == 1 && rays == SLG_RAYS_PINHOLE && row_mode == 0) {
+    SLG_PCASE(0, 0, SLG_PLAN_C1) SLG_PCASE(0, 1, SLG_PLAN_C1)
+    SLG_PCASE(0, 0, SLG_PLAN_C1 | kPlanGray) SLG_PCASE(0, 1, SLG_PLAN_C1 | kPlanGray)
 #undef SLG_PCASE
   }
 #endif
@@ -2565,7 +2685,8 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
     for (int k = 0; k < mp.n_views; ++k) {
       Plan pl;
       make_plan(&caps[v0 + k], dp, &pl);
-      const int key = pl.col_pairs <= 15 && pl.row_pairs <= 15 ? (pl.col_pairs << 4) | pl.row_pairs : 0;
+      const int rp = tp->row_mode == 0 ? 0 : pl.row_pairs;     // row_mode 0 reads no row frame
+      const int key = pl.col_pairs <= 15 && rp <= 15 ? (pl.col_pairs << 4) | rp : 0;
       plan = plan < 0 || plan == key ? key : 0;
       all_gray = all_gray && !caps[v0 + k].texture;
       any_gray = any_gray || !caps[v0 + k].texture;

@@ -121,6 +121,30 @@ HOST_AHEAD = 12
 DEVICE_MAX_VIEWS = 16
 
 
+_DECODE_STREAMS: dict = {}
+
+
+def png_decode_stream(device: int | None = None):
+    """The device PNG decode's stream, one per GPU for the process: every ``SLG_PNG_RESERVE_EVERY``
+    -th CU (default 16th) left out of its CU mask (``slg_stream_create_reserving``), so the
+    ~225 ms inflate launch leaves 16 of 256 CUs to the fused launches of the host-decoded views
+    (their 72 KB of LDS per workgroup fit on no CU the inflate's 50 KB waves hold); a plain
+    stream when the mask cannot be set.  240 CUs x 3 inflate waves still hold a 16-view group's
+    704 streams at once."""
+    dev = torch.cuda.current_device() if device is None else int(device)
+    s = _DECODE_STREAMS.get(dev)
+    if s is None:
+        every = int(os.environ.get("SLG_PNG_RESERVE_EVERY", "16"))
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            if every >= 2 and N.lib().slg_stream_create_reserving(every, ctypes.byref(h)) == 0:
+                s = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", dev))
+            else:
+                s = torch.cuda.Stream(device=dev)
+        _DECODE_STREAMS[dev] = s
+    return s
+
+
 def device_share(n_folders: int, mode: str | None = None) -> int:
     """Folders (the last ones of the batch) whose PNG frames the GPU decodes."""
     mode = device_png_mode() if mode is None else mode
@@ -406,26 +430,27 @@ class BatchPipeline:
 
     PNG decode is split between the host threads and the GPU (:func:`device_share`): the last
     folders of the batch are read as zlib streams and decoded by ONE device launch issued at the
-    start, on a stream of its own, while the host threads decode the others; the device group is
-    reconstructed when the pipeline reaches it, in folder order.  PLY files are written by
-    ``writers`` threads (a C2 view's ASCII PLY is ~60 MB)."""
+    start, on a stream of its own that leaves CUs free (:func:`png_decode_stream`), while the host
+    threads decode the others; the device group is reconstructed when the pipeline reaches it,
+    in folder order.  PLY files are written by ``writers`` threads (a C2 view's ASCII PLY is
+    ~60 MB; profiles/r5e: one writer thread bounded the round-4 pipeline)."""
 
     def __init__(self, cfg: E.DecodeConfig, calib: dict, row_mode=1, epipolar_tol=2.0, group: int = 8,
                  depth: int | None = None, log=print, order=("bmp", "png"), device_ply: bool = True,
-                 writers: int = 4, device_views: int | None = None):
+                 writers: int | None = None, device_views: int | None = None):
         if row_mode not in (0, 1, 2):
             raise ValueError("row_mode must be 0, 1 or 2")
         self.cfg, self.calib, self.row_mode, self.tol = cfg, calib, int(row_mode), float(epipolar_tol)
         self.group = max(1, min(int(group), E.MAX_VIEWS_PER_LAUNCH))
-        self.depth = depth or max(2 * self.group, 16)
+        self._depth = depth                          # None: max(2 group, 16), 24 beside a device group
         self.log, self.order = log, order
-        self.writers = max(1, int(writers))
+        self.writers = max(1, int(writers if writers is not None else os.environ.get("SLG_PLY_WRITERS", 8)))
         self.device_views = device_views          # None: device_share() of the batch
         self.pool = PinnedPool()
         self.copy_stream = torch.cuda.Stream()
         self.compute_stream = torch.cuda.Stream()
         self.format_stream = torch.cuda.Stream()     # PLY bodies of group k beside group k+1's kernels
-        self.decode_stream = torch.cuda.Stream()     # the device-decoded group's H2D + inflate
+        self.decode_stream = png_decode_stream()     # the device-decoded group's H2D + inflate
         self.formatter = PLY.DeviceFormatter()
         self.device_ply = device_ply
         self.engines: dict = {}
@@ -600,6 +625,9 @@ class BatchPipeline:
             n_dev = 0                               # every group is read for the device decoder
         if n_dev:
             self._max_views = max(self.group, n_dev)
+        # read-ahead: the host keeps decoding while the device group's inflate holds most CUs
+        self.depth = self._depth or int(os.environ.get("SLG_PIPE_DEPTH", 0)) or (
+            max(2 * self.group, 24) if n_dev else max(2 * self.group, 16))
         dev_first = len(order) - n_dev              # the device group: the last n_dev image folders
         cut = len(entries)
         if n_dev:

@@ -218,3 +218,59 @@ def test_pipeline_falls_back_to_host_for_a_refused_frame(tmp_path, N, monkeypatc
             os.remove(os.path.join(f, os.path.basename(f) + ".ply"))
     assert refused == [folders[1]]
     assert outs["1"] == outs["0"] and all(len(b) > 1000 for b in outs["1"])
+
+
+def test_pipeline_group_upload_failure_falls_back_per_view(tmp_path, N, monkeypatch):
+    """A group upload that raises after its device decode was queued (the frame
+    buffers must not be reused while that work still writes them): the pipeline waits for the
+    queued work, decodes the group's views again on the host one by one, and writes the same PLY
+    bytes as a host-only run.  Also the hybrid split (SLG_PNG_DEVICE unset: the last folders on
+    the device decoder, the rest on host threads) writes the same bytes."""
+    from structured_light_for_3d_model_replication_amd import calibration, synth
+    from structured_light_for_3d_model_replication_amd import pipeline as PL
+    from structured_light_for_3d_model_replication_amd import processing as PR
+    rig = synth.default_rig(320, 240, 1920, 1080)
+    root = tmp_path / "scan"
+    folders = []
+    for i in range(6):
+        v = synth.render_view(rig, 60.0 * i, seed=30 + i, n_present=46)
+        f = str(root / f"v{i}")
+        synth.write_capture(v, f)
+        folders.append(f)
+    calib = str(tmp_path / "calib.mat")
+    calibration.save_mat(calib, rig.tables())
+    real = PL.decode_png_device
+    failed = []
+
+    def fail_after_queueing(pngs, stream):
+        real(pngs, stream)                           # the inflate launch is queued ...
+        failed.append(len(pngs))
+        raise RuntimeError("injected mid-group failure")   # ... and the group upload raises
+
+    def run(env, group, patch=False, ahead=None):
+        monkeypatch.setenv("SLG_BATCH_VIEWS", str(group))
+        if env is None:
+            monkeypatch.delenv("SLG_PNG_DEVICE", raising=False)
+        else:
+            monkeypatch.setenv("SLG_PNG_DEVICE", env)
+        if ahead is not None:
+            monkeypatch.setenv("SLG_PNG_HOST_AHEAD", str(ahead))
+        monkeypatch.setattr(PL, "decode_png_device", fail_after_queueing if patch else real)
+        logs = []
+        PR.ProcessingLogic.process_multi_ply(calib, str(root), "batch", log_callback=logs.append)
+        out = [open(os.path.join(f, os.path.basename(f) + ".ply"), "rb").read() for f in folders]
+        for f in folders:
+            os.remove(os.path.join(f, os.path.basename(f) + ".ply"))
+        assert logs[-1] == "=== Batch Complete: 6/6 succeeded ===", logs[-3:]
+        return out, PL.LAST_STATS.as_dict()
+
+    host, st = run("0", 3)
+    assert st["folders_device_decoded"] == 0 and all(len(b) > 1000 for b in host)
+    fell, _ = run("1", 3, patch=True)                # every group's device upload fails
+    assert failed == [3, 3] and fell == host
+    hybrid, st = run(None, 2, ahead=2)               # auto: 4 folders on the device, 2 on the host
+    assert st["folders_device_decoded"] == 4 and st["folders_host_decoded"] == 2, st
+    assert hybrid == host
+    failed.clear()
+    fell2, st = run(None, 2, patch=True, ahead=2)    # the device group's upload fails: host redo
+    assert failed == [4] and fell2 == host

@@ -34,7 +34,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--views", type=int, default=36)
     ap.add_argument("--runs", default="host:1,host:4,host:8,auto:4,auto:8,device:16",
-                    help="comma list of decoder:group (decoder host | auto | device)")
+                    help="comma list of decoder:group[:NAME=VAL+NAME=VAL] (decoder host | auto | device; "
+                         "extra environment for that run, e.g. auto:8:SLG_PNG_RESERVE_EVERY=0)")
     ap.add_argument("--reps", type=int, default=1, help="repetitions of the whole list (interleaved)")
     ap.add_argument("--parts", action="store_true", help="also the serial per-stage costs")
     ap.add_argument("--out", default="", help="also write the JSON here")
@@ -60,17 +61,27 @@ def main():
         folders = [f.path for f in os.scandir(root) if f.is_dir()]     # the order batch mode uses
         kw = dict(n_sets_col=11, n_sets_row=10)
         PR.ProcessingLogic.process_multi_ply(calib, folders[0], "single", log_callback=lambda m: None, **kw)  # warm-up
-        runs = [r.split(":") for r in args.runs.split(",") if r]
+        runs = [(r.split(":") + [""])[:3] for r in args.runs.split(",") if r]
         res, plys = {}, {}
         env = {"host": "0", "auto": "auto", "device": "1"}
         for rep in range(args.reps):
-            for dec, g in runs:
+            for dec, g, extra in runs:
                 os.environ["SLG_PNG_DEVICE"] = env[dec]
                 os.environ["SLG_BATCH_VIEWS"] = g
+                saved = {}
+                for kv in filter(None, extra.split("+")):
+                    k, _, v = kv.partition("=")
+                    saved[k] = os.environ.get(k)
+                    os.environ[k] = v
                 t0 = time.perf_counter()
                 PR.ProcessingLogic.process_multi_ply(calib, root, "batch", log_callback=lambda m: None, **kw)
                 dt = time.perf_counter() - t0
-                key = f"{dec}_group{g}"
+                for k, v in saved.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+                key = f"{dec}_group{g}" + (f"_{extra}" if extra else "")
                 st = PL.LAST_STATS.as_dict()
                 res.setdefault(key, []).append({"s_per_view": round(dt / args.views, 4), **st})
                 print(f"[e2e] rep {rep} {key}: {dt / args.views:.4f} s/view {st}", file=sys.stderr, flush=True)

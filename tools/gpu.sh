@@ -57,9 +57,13 @@ for step in "$@"; do
       if [ -n "$rest" ]; then
         pname=${rest%%=*}; pargs=${rest#*=}
         PMC_TIMEOUT=300 BENCH_ARGS="${pargs//,/ }" bash "$R/tools/gpu_profile.sh" "$TAG/prof_$pname" || { echo "[gpu.sh] PROF $pname FAILED"; exit $n; }
+        pdir=$O/prof_$pname
       else
         bash "$R/tools/gpu_profile.sh" "$TAG/prof" || { echo "[gpu.sh] PROF FAILED"; exit $n; }
-      fi ;;
+        pdir=$O/prof
+      fi
+      # the raw traces run to tens of MB; gpurun copies back at most 64 MiB per call
+      find "$pdir" -name "*.csv" -size +512k -exec gzip -f {} \; ;;
     sq)
       bash "$R/tools/pmc_main.sh" "$TAG/sq" || { echo "[gpu.sh] SQ FAILED"; exit $n; } ;;
     ab)

@@ -74,6 +74,14 @@ def main():
         print(name, r, file=sys.stderr, flush=True)
 
     run("stats", lambda v: eng.stats(dfr[v], cfg))
+    os.environ["SLG_DBG"] = "16"                     # Otsu replaced by a constant: the tail's share
+    run("stats_no_otsu", lambda v: eng.stats(dfr[v], cfg))
+    os.environ.pop("SLG_DBG")
+    # one view's whole drop-in call (_gray_decode + _reconstruct_point_cloud fused): stats + main
+    # in one event pair, f32 and the drop-in's f64
+    for tag, x64 in (("", False), ("_f64", True)):
+        solo_out = E.Cloud(H * W, 1, x64)
+        run(f"solo_rm1{tag}", lambda v, o=solo_out: eng.reconstruct(dfr[v], cfg, dcal, 1, 2.0, out=o))
     pts = {}
     for rm in (0, 1, 2):
         def f(v, rm=rm):

@@ -17,6 +17,7 @@ from __future__ import annotations
 import argparse
 import collections
 import csv
+import gzip
 import json
 import os
 import shutil
@@ -27,6 +28,9 @@ LANES = 512                      # main3 workgroup (kTileBlock)
 
 
 def rows_of(path, kernel):
+    if not os.path.exists(path) and os.path.exists(path + ".gz"):    # (tools/gpu.sh gzips big traces)
+        with gzip.open(path + ".gz", "rt") as f:
+            return [r for r in csv.DictReader(f) if kernel in r["Kernel_Name"]]
     if not os.path.exists(path):
         return []
     with open(path) as f:
