@@ -71,7 +71,7 @@ struct WsHeader {
   uint32_t max_diff_enc;   // max(white-black) + 256 (0 = none yet)
   uint32_t ticket;         // stats_kernel arrival counter
   uint32_t tile_counter;   // next (view, tile) id of a main3 launch (this slice = its view 0)
-  uint32_t error;          // bit 0: look-back spin timeout
+  uint32_t error;          // bit 0: look-back spin timeout; 1: a look-back helper ran; 2: SOLO threshold wait gave up
   int32_t smin;            // mask: white >= smin
   int32_t cmin;            //       (white - black) >= cmin
   int32_t pad0[2];
@@ -82,7 +82,10 @@ struct WsHeader {
   // which the clipped histogram cannot count); their minimum bounds the valid pixels, so the
   // point count of row_mode 0/1 (resident jobs size their clouds with it).  n_px otherwise.
   int64_t above[2];
-  uint64_t pad3[6];
+  // one-view fused launches (main3 SOLO): [0] chunk claims, [1] chunks counted, [2] workgroups
+  // exited, [3] thresholds ready; the launch's last workgroup to exit zeroes them again
+  uint32_t solo[4];
+  uint64_t pad3[4];
 };
 constexpr int kHistCopies = 16;            // partial histograms: blocks spread their atomics
 constexpr int64_t kHistPartOff = 8192;      // uint32 [kHistCopies][2][256] after the header
@@ -284,8 +287,8 @@ __device__ __attribute__((always_inline)) inline int64_t hist_at_least_wave(cons
 #define SLG_OTSU_MARK(k)                   // tools/otsu_probe.hip: a timestamp per part of otsu_wave
 #endif
 #ifndef SLG_OTSU_LDS
-#define SLG_OTSU_LDS 1                     // the chains fed from LDS (0: the round-4 readlane chains)
-#endif
+#define SLG_OTSU_LDS 3                     // 3: broadcast LDS operands + v_cndmask capture (both chains);
+#endif                                     // 2: q1 by readlanes, mu1 from LDS; 1: both LDS-stored; 0: readlanes (round 4)
 constexpr int kOtsuLds = 7 * 256 + 128;   // 7 arrays of 256 bins + the chains' dump words
 constexpr int kOtsuChunk = 8;
 
@@ -308,29 +311,36 @@ __device__ __attribute__((always_inline)) inline void q1_chain_lds(const double*
   }
 }
 
-// mu1_run<true> on LDS operands: over bins [lo, hi], a = mu1 * q1[i-1] + ip[i] (mu1 = 0 at lo,
-// where q1[lo-1] is taken as 0 as mu1_run does), mu1 = fma(a, y[i], a * c[i]) with
-// c[i] = fma(-q1[i], y[i], 1) * y[i] precomputed; every bin's a and mu1 stored for the check
+// mu1_run<true> on LDS operands, over bins [lo, hi]: a = mu1 * q1[i-1] + ip[i] (mu1 = 0 at lo,
+// where q1[lo-1] is taken as 0 as mu1_run does) as the reference rounds it, then
+// mu1 = fma(a, y[i], e) with e = fma(mu1, qc[i], ipc[i]) ~ a * c[i] (qc = q1[i-1] c, ipc = ip c,
+// c = fma(-q1, y, 1) y, all precomputed): e is only the ~2^-53-relative correction of a y, so
+// computing it from mu1 instead of from the rounded a changes the result only where a / q1 lies
+// within ~2^-104 of a rounding boundary, which the caller's check catches.  Three dependent fp64
+// ops per bin (mul, add, fma) instead of four.  Every bin's a and mu1 stored for the check
 // (branch-free, as q1_chain_lds).
 __device__ __attribute__((always_inline)) inline void mu1_chain_lds(int lo, int hi, const double* sq, const double* sip,
-                                                                    const double* sy, const double* sc, double* sa,
-                                                                    double* sm, double* dump) {
+                                                                    const double* sy, const double* sqc,
+                                                                    const double* sipc, double* sa, double* sm,
+                                                                    double* dump) {
   const int lane = threadIdx.x & 63;
   constexpr int C = 4;
   double mu1 = 0.0;
 #pragma unroll 1
   for (int i0 = lo; i0 <= hi; i0 += C) {
-    double qp[C], ipk[C], yk[C], ck[C];
+    double qp[C], ipk[C], yk[C], qck[C], ipck[C];
 #pragma unroll
     for (int k = 0; k < C; ++k) {
       const int i = i0 + k <= hi ? i0 + k : hi;        // (past hi: computed, never stored)
       qp[k] = i > lo ? sq[i - 1] : 0.0;
-      ipk[k] = sip[i]; yk[k] = sy[i]; ck[k] = sc[i];
+      ipk[k] = sip[i]; yk[k] = sy[i]; qck[k] = i > lo ? sqc[i] : 0.0; ipck[k] = sipc[i];
     }
 #pragma unroll
     for (int k = 0; k < C; ++k) {
-      const double a = mu1 * qp[k] + ipk[k];
-      mu1 = fma(a, yk[k], a * ck[k]);
+      const double m = mu1 * qp[k];
+      const double e = fma(mu1, qck[k], ipck[k]);
+      const double a = m + ipk[k];
+      mu1 = fma(a, yk[k], e);
       const bool mine = lane == 0 && i0 + k <= hi;
       *(mine ? sa + i0 + k : dump + lane) = a;
       *(mine ? sm + i0 + k : dump + 64 + lane) = mu1;
@@ -347,9 +357,10 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
   double* sq = lds + 256;           // q1_i
   double* sip = lds + 512;          // i * p_i
   double* sy = lds + 768;           // RN(1 / q1_i) of unskipped bins
-  double* sc = lds + 1024;          // fma(-q1_i, y_i, 1) * y_i
+  double* sqc = lds + 1024;         // q1_{i-1} * c_i, c_i = fma(-q1_i, y_i, 1) * y_i
   double* sa = lds + 1280;          // the mu1 chain's numerators
   double* sm = lds + 1536;          // and its mu1 values
+  double* sipc = lds;               // ip_i * c_i (over p_i, which only the q1 chain reads)
   double pv[4], ip[4], q1r[4], yr[4], m1r[4], ar[4];
   uint64_t isum = 0;
 #pragma unroll
@@ -367,7 +378,32 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
   SLG_OTSU_MARK(1);
   // 1. the q1 chain (OpenCV's order): LDS in, LDS out (wave-local: the wave's own LDS ops are
   // in order, the fence only keeps the compiler from moving them)
-#if SLG_OTSU_LDS
+#if SLG_OTSU_LDS == 3
+  // operands as broadcast LDS reads, each bin's result captured into its owner lane's register
+  // by v_cndmask: a dependent fp64 op costs ~5 clocks (tools/dp_latency_probe.hip), so a bin's
+  // cost is its instruction count -- here one add and two selects
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    double q1 = 0.0;
+#pragma unroll 1
+    for (int l0 = 0; l0 < 64; l0 += 4) {
+      double pp[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) pp[k] = sp[4 * l0 + k];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bool mine = lane == l0 + t;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          q1 = q1 + pp[4 * t + j];
+          q1r[j] = mine ? q1 : q1r[j];
+        }
+      }
+    }
+  }
+#elif SLG_OTSU_LDS == 1
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   q1_chain_lds(sp, sq, lds + 7 * 256);
@@ -377,7 +413,9 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
 #pragma unroll
   for (int j = 0; j < 4; ++j) q1r[j] = sq[4 * lane + j];
 #else
-  double q1 = 0.0;                                   // (the readlane chain, for A/B)
+  // the readlane chain: 36 clocks per bin against 51 for q1_chain_lds (tools/otsu_probe.hip,
+  // profiles/r5g) -- its operand and result moves are independent of the chain
+  double q1 = 0.0;
   for (int l = 0; l < 64; ++l) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -386,6 +424,8 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
       q1 = nq;
     }
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sq[4 * lane + j] = q1r[j];
 #endif
   SLG_OTSU_MARK(2);
   uint32_t okr = 0;                                  // 2. bit j: bin 4*lane+j not skipped
@@ -396,9 +436,20 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
       okr |= 1u << j;
       yr[j] = 1.0 / q1r[j];
     }
-    sy[4 * lane + j] = yr[j];
-    sc[4 * lane + j] = fma(-q1r[j], yr[j], 1.0) * yr[j];
   }
+#if SLG_OTSU_LDS == 1 || SLG_OTSU_LDS == 2
+  {                                                  // the mu1 chain's precomputed operands
+    const double q_last_prev = __shfl_up(q1r[3], 1); // q1 of bin 4 lane - 1 (lane 0: unused)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double c = fma(-q1r[j], yr[j], 1.0) * yr[j];
+      const double qprev = j == 0 ? q_last_prev : q1r[j - 1];
+      sy[4 * lane + j] = yr[j];
+      sqc[4 * lane + j] = qprev * c;
+      sipc[4 * lane + j] = ip[j] * c;
+    }
+  }
+#endif
   // 3. the mu1 chain.  The unskipped bins form one run [lo, hi]: q1 never decreases and
   // q2 = RN(1 - q1) never increases, so each skip test holds on a prefix plus a suffix of the
   // bins, and mu1 is still 0 at lo.  Over the run every bin is the same 4 dependent ops
@@ -419,11 +470,45 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
   double mu1 = 0.0;
   SLG_OTSU_MARK(4);
   if (n_ok == hi - lo + 1 && n <= (int64_t(1) << 52)) {
-#if SLG_OTSU_LDS
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#if SLG_OTSU_LDS == 3
+    {                                                // per bin {q1[i-1], ip, y, c}, 32 bytes
+      double* sops = lds + 256;
+      const double qprev0 = __shfl_up(q1r[3], 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double* o = sops + 4 * (4 * lane + j);
+        o[0] = j == 0 ? qprev0 : q1r[j - 1];
+        o[1] = ip[j];
+        o[2] = yr[j];
+        o[3] = fma(-q1r[j], yr[j], 1.0) * yr[j];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double mu1c = 0.0;                             // = mu1_run<true>: 0 at lo, whatever q1[lo-1]
+#pragma unroll 1
+      for (int l = lo >> 2; l <= (hi >> 2); ++l) {
+        double o[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) o[k] = sops[16 * l + k];
+        const bool mine = lane == l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * l + j;
+          const bool act = i >= lo && i <= hi;       // wave-uniform
+          const double a = mu1c * o[4 * j] + o[4 * j + 1];
+          const double m = fma(a, o[4 * j + 2], a * o[4 * j + 3]);
+          mu1c = act ? m : mu1c;
+          m1r[j] = (mine && act) ? m : m1r[j];
+          ar[j] = (mine && act) ? a : ar[j];
+        }
+      }
+    }
+#elif SLG_OTSU_LDS
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // (1, 2: the mu1 chain from LDS)
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    mu1_chain_lds(lo, hi, sq, sip, sy, sc, sa, sm, lds + 7 * 256);   // = mu1_run<true>(lo, hi, ...)
+    mu1_chain_lds(lo, hi, sq, sip, sy, sqc, sipc, sa, sm, lds + 7 * 256);   // ~ mu1_run<true>(lo, hi, ...)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -986,12 +1071,31 @@ struct NoPre {
 // Constant counts make every frame load unconditional, so the decode consumes each pair as it
 // lands (vmcnt(n) in issue order) instead of after a vmcnt(0) for the whole batch, and drop the
 // per-pair branches (243.3 vs 259.8 us per 12-view launch, profiles/r3m).
-template <int ROW_MODE, int SRC_FRAMES, int kBatch, bool MF = false, int PLAN = 0, class Pre = NoPre>
+// One-view fused launches (SOLO): the thresholds come from the workgroups of the same launch
+// (solo_stats); a wave waits for them only once its frame loads are issued.
+__device__ inline void solo_wait(WsHeader* ws) {
+  // relaxed polls (an agent-scope acquire load invalidates the L2 on every poll: with ~4000
+  // waves polling that made the one-view launch 580 us, profiles/r5k)
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(&ws->solo[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+    __builtin_amdgcn_s_sleep(8);
+    // (cannot happen -- solo_stats always raises the flag; but a kernel must end: after 50 ms
+    // flag the error, bit 2, and go on; reconstruct_view refuses such a cloud)
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+      atomicOr(&ws->error, 4u);
+      break;
+    }
+  }
+}
+
+template <int ROW_MODE, int SRC_FRAMES, int kBatch, bool MF = false, int PLAN = 0, class Pre = NoPre, bool SOLO = false>
 __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, uint32_t& valid,
                                    int (&col)[kPx], int (&row)[kPx], Pre pre = Pre()) {
   valid = 0;
   if (SRC_FRAMES) {
-    const int smin = p.ws->smin, cmin = p.ws->cmin;
+    static_assert(!(SOLO && MF), "a one-view launch decodes densely: its mask waits for the thresholds");
+    int smin = 0, cmin = 0;
+    if constexpr (!SOLO) { smin = p.ws->smin; cmin = p.ws->cmin; }
     const int64_t lp = px0 < p.n_px ? px0 : 0;
     const uint2 w = ld_frame8(p, 0, lp);
     const uint2 bl = ld_frame8(p, 1, lp);
@@ -1043,6 +1147,17 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
     uint32_t ac[4], ar[4];
     acc_codes(qc, np_c, p.col_pre, p.col_post, ac);
     acc_codes(qr, np_r, p.row_pre, p.row_post, ar);
+    if constexpr (SOLO) {                           // every frame load issued: now the thresholds
+      // one lane per workgroup polls (every wave polling put thousands of uncached loads a
+      // microsecond on the memory system: 170 us per one-view launch, profiles/r5l)
+      // what the thresholds' workgroup wrote and the waves read next -- smin, cmin, the zeroed
+      // look-back words -- is read by agent-scope atomics, so no cache invalidation is needed
+      if (threadIdx.x == 0) solo_wait(p.ws);
+      __syncthreads();
+      smin = __hip_atomic_load(&p.ws->smin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      cmin = __hip_atomic_load(&p.ws->cmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pre(w);                                       // (a gray capture's colour: the white bytes)
+    }
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
       if constexpr (!MF) {
@@ -1559,7 +1674,7 @@ struct Main3Params {
   int32_t n_views;
   int32_t n_fin;              // views finished by this launch (FinIO), 0: none
   int32_t fin_blocks;         // finishing workgroups per such view (the grid's first n_fin*fin_blocks)
-  int32_t pad;
+  int32_t solo;               // one-view launch counting its own Otsu histograms (main3 SOLO)
   int64_t n_state_words;      // look-back words per view slice (finishing arms them)
   int64_t pad_zero;           // zero bytes the last tile's partial counted past n_px
   ViewIO v[kMaxViews];
@@ -1811,11 +1926,111 @@ __device__ inline void tri_rounds(const MainParams& p, int i, int n_items, const
   tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt, NP, NC>(p, i, n_items, s_item, pts, km);
 }
 
+// The Otsu stats of a one-view fused launch (SOLO), done by the launch's own workgroups before
+// their tiles: each claims 4096-pixel chunks of the view (ws->solo[0]) until none is left,
+// histograms a chunk on the matrix cores (the carried-histogram code, hist_next_*), adds it to
+// the view's histogram copies and takes a ticket (ws->solo[1]); the workgroup counting the last
+// chunk sums the copies, runs Otsu (otsu_wave, as stats_kernel), arms the look-back words and
+// raises ws->solo[3].  No workgroup waits before it has claimed past the last chunk, and every
+// claimed chunk belongs to a running workgroup that waits for nothing, so the flag always comes:
+// whatever order the workgroups are dispatched in, the launch cannot deadlock.
+__device__ __attribute__((always_inline)) inline void solo_stats(const MainParams& p, int64_t n_tiles,
+                                                                 int64_t n_state_words, int64_t pad_zero,
+                                                                 uint2* s_hstage, uint32_t* s_hn, uint32_t* s_lds,
+                                                                 int* s_flag) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  WsHeader* ws = p.ws;
+  uint32_t* hist_part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + kHistPartOff);
+  for (;;) {
+    if (tid == 0) *s_flag = int(atomicAdd(&ws->solo[0], 1u));
+    __syncthreads();
+    const int64_t c = *s_flag;
+    __syncthreads();
+    if (c >= n_tiles) break;
+    const int64_t o = c * kTilePx + int64_t(tid) * kPx;
+    uint2 wq, bq;
+    hist_next_load(p.frames, p.frames + p.stride, p.n_px, o, wq, bq);
+    for (int i = tid; i < 512; i += kTileBlock) s_hn[i] = 0;
+    hist_next_stage(wq, bq, p.n_px, o, s_hstage);
+    __syncthreads();
+    hist_next_count(s_hstage, s_hn, wave, kTileBlock / 64);
+    __syncthreads();
+    for (int i = tid; i < 512; i += kTileBlock) {
+      const uint32_t v = s_hn[i];
+      if (v) atomicAdd(hist_part + (c % kHistCopies) * 512 + i, v);
+    }
+    // the chunk's counts are agent-scope atomics: complete (vmcnt) before the ticket, no L2
+    // write-back (an agent-scope release fence is a buffer_wbl2 of the whole L2: one per
+    // workgroup and chunk made the one-view launch ~160 us, profiles/r5l)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t d = __hip_atomic_fetch_add(&ws->solo[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *s_flag = d == uint32_t(n_tiles - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (*s_flag) {                                   // the last chunk: thresholds for the launch
+      if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __syncthreads();
+      uint32_t* hg = s_lds;
+      for (int i = tid; i < 512; i += kTileBlock) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < kHistCopies; ++k)
+          acc += __hip_atomic_load(hist_part + k * 512 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((i & 255) == 0) acc -= uint32_t(pad_zero);   // zero bytes staged past n_px
+        hg[i] = acc;
+      }
+      __syncthreads();
+      if (wave < 2) {                                // wave 0: white, wave 1: clip(w-b)
+        const double thr = otsu_wave(hg + 256 * wave, p.n_px, reinterpret_cast<double*>(s_lds + 512) + wave * kOtsuLds);
+        const int m = int_threshold(thr, wave == 0 ? 0 : -255);
+        const int64_t above = hist_at_least_wave(hg + 256 * wave, m, p.n_px);
+        if (lane == 0) {
+          if (wave == 0) {
+            __hip_atomic_store(&ws->smin, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ws->thr_s = thr;
+          } else {
+            __hip_atomic_store(&ws->cmin, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ws->thr_c = thr;
+          }
+          ws->above[wave] = above;
+        }
+      }
+      uint64_t* states = p.states;
+      for (int64_t i = tid; i < n_state_words; i += kTileBlock) states[i] = 0;   // arm the look-back
+      for (int i = tid; i < kHistCopies * 512; i += kTileBlock) hist_part[i] = 0;
+      if (tid == 0) { ws->solo[1] = 0; ws->tile_counter = 0; }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(&ws->solo[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// The last workgroup of a one-view fused launch to leave resets the SOLO words for the next one
+// (atomics only: every workgroup's uses of them are atomics, done before its exit ticket).
+__device__ inline void solo_exit(WsHeader* ws, int n_wg) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t e = __hip_atomic_fetch_add(&ws->solo[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e == uint32_t(n_wg - 1)) {
+      __hip_atomic_store(&ws->solo[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ws->solo[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ws->solo[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // PROF: the profiling instance (SLG_DBG set): honours the ablation bits of MainParams::dbg and
 // writes per-workgroup phase records; the production instances carry none of that code.
 constexpr int kPlanGray = 0x100;           // PLAN bit: every view of the launch is a gray capture
 
-template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS, bool PROF, int PLAN = 0>
+template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS, bool PROF, int PLAN = 0, bool SOLO = false>
 __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) void main3_kernel(Main3Params P) {
   using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
   constexpr int NS = ROW_MODE == 2 ? 2 : 1;
@@ -1863,6 +2078,8 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // look-back, D stores (100 MHz ticks), look-back polls, sleep units, items, start} written to
   // view 0's partials region (tools/kbench.py "phases"; the host refuses it when a batch is
   // carried, whose partials live there).
+  if constexpr (SOLO)                                // the view's thresholds, counted right here
+    solo_stats(p, tiles, P.n_state_words, P.pad_zero, s_hstage, s_hn, reinterpret_cast<uint32_t*>(s_item), &s_wtot[0]);
   const bool prof = PROF && (p.dbg & 64) != 0;
   uint64_t t_phase = prof ? __builtin_amdgcn_s_memrealtime() : 0;
   // the record lives in LDS (tid 0 writes it): as a register array it pushed the profiling
@@ -1926,11 +2143,17 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
           if (px0 * 3 + k < p.n_px * 3) tex[k >> 2] |= uint32_t(p.texture[px0 * 3 + k]) << (8 * (k & 3));
       }
     };
-    constexpr bool MF = SLG_MASK_FIRST && SRC_FRAMES;
-    if (!SLG_TEX_LATE && !MF) load_tex(make_uint2(0u, 0u));   // (gray needs MF: host check)
+    constexpr bool MF = SLG_MASK_FIRST && SRC_FRAMES && !SOLO;
+    if (!SLG_TEX_LATE && !MF && !(SOLO && gray)) load_tex(make_uint2(0u, 0u));   // (gray: MF or SOLO)
     uint32_t valid;
     int col[kPx], row[kPx];
-    if constexpr (MF) {
+    if constexpr (SOLO) {
+      // one view: every frame read densely while the thresholds are being counted; a gray
+      // capture's colour comes from the white bytes once they are known to be needed
+      auto pre_gray = [&](uint2 w) { if (gray) load_tex(w); };
+      decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH, false, PLAN, decltype(pre_gray), true>(p, px0, tail, valid, col,
+                                                                                             row, pre_gray);
+    } else if constexpr (MF) {
       // mask first: a lane with a valid pixel issues its texture loads, then its pattern loads
       decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH, true, PLAN>(p, px0, tail, valid, col, row, load_tex);
     } else {
@@ -1938,7 +2161,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     }
     // SLG_TEX_LATE: only lanes with a valid pixel read their 24 texture bytes, once the mask is
     // known (the block scan's barrier covers part of the latency)
-    if (!MF && SLG_TEX_LATE && valid != 0u) load_tex(make_uint2(0u, 0u));
+    if (!MF && SLG_TEX_LATE && valid != 0u && !(SOLO && gray)) load_tex(make_uint2(0u, 0u));
     const int2 sc = block_scan(__popc(valid), s_wtot);
     n_items = sc.y;
     int m = sc.x;
@@ -2232,6 +2455,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       if (!(PROF && (p.dbg & 8)))
         bgr_tile_store(s == 0 ? p.bgr : p.scratch_bgr, int64_t(s_excl[s]), s_agg[s], s_stage + s * kStageWords);
   }
+  if constexpr (SOLO) solo_exit(p.ws, int(gridDim.x));
   if (prof) {
     __syncthreads();
     stamp(3);
@@ -2555,7 +2779,17 @@ using Main3Fn = void (*)(Main3Params);
 #define SLG_PLAN_C1 0xA0           // row_mode 0, 10 column bits (1024-wide projector), no row pairs
 
 template <int SRC>
-Main3Fn pick_main(int row_mode, int x64, int rays, int plan = 0) {
+Main3Fn pick_main(int row_mode, int x64, int rays, int plan = 0, bool solo = false) {
+#ifndef SLG_FAST_BUILD
+  if (SRC == 1 && solo && !(debug_flags() & kMainDbgBits)) {   // one-view launches with in-launch stats
+#define SLG_SCASE(RM, X, R) if (row_mode == RM && x64 == X && rays == R) return main3_kernel<RM, X, 1, R, false, 0, true>;
+    SLG_SCASE(0, 0, 0) SLG_SCASE(0, 0, 1) SLG_SCASE(0, 1, 0) SLG_SCASE(0, 1, 1)
+    SLG_SCASE(1, 0, 0) SLG_SCASE(1, 0, 1) SLG_SCASE(1, 1, 0) SLG_SCASE(1, 1, 1)
+    SLG_SCASE(2, 0, 0) SLG_SCASE(2, 0, 1) SLG_SCASE(2, 1, 0) SLG_SCASE(2, 1, 1)
+#undef SLG_SCASE
+    return nullptr;
+  }
+#endif
   if (debug_flags() & kMainDbgBits) {
     if (!(SRC == 1 && row_mode == 1 && x64 == 0 && rays == SLG_RAYS_PINHOLE)) return nullptr;
     return plan == SLG_PLAN_C2 ? main3_kernel<1, 0, 1, 1, true, SLG_PLAN_C2> : main3_kernel<1, 0, 1, 1, true>;
@@ -2642,7 +2876,7 @@ int check_batch(const slg_capture* caps, int n_views) {
 int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* dp, const slg_calib* calib,
                 const slg_tri_params* tp, char* ws, int64_t ws_stride, const slg_cloud* outs,
                 void* const* timing_events, hipStream_t s, const slg_capture* next = nullptr, int n_next = 0,
-                char* fin_ws = nullptr, int n_fin = 0) {
+                char* fin_ws = nullptr, int n_fin = 0, bool solo = false) {
   if (!caps || n_views < 1 || !dp || !ws || !outs) return fail(SLG_ERR_INVALID, "NULL argument");
   int rc = check_batch(caps, n_views);
   if (rc) return rc;
@@ -2693,7 +2927,7 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
     }
     // a mixed launch runs the generic instance (per-view test); a plan instance is all one kind
     if (plan > 0 && any_gray) plan = all_gray ? (plan | kPlanGray) : 0;
-    const Main3Fn fn = pick_main<1>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode, plan < 0 ? 0 : plan);
+    const Main3Fn fn = pick_main<1>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode, plan < 0 ? 0 : plan, solo);
     for (int k = 0; k < mp.n_views; ++k) {
       const int v = v0 + k;
       ViewIO& io = mp.v[k];
@@ -2714,6 +2948,11 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
       }
     }
     mp.n_fin = launch == 0 ? n_fin : 0;             // the first launch finishes them all
+    if (solo) {                                     // (one view, Otsu: fused_solo)
+      mp.solo = 1;
+      mp.n_state_words = n_state_words(n_px);
+      mp.pad_zero = mp.c.n_tiles * kTilePx - n_px;
+    }
     if (mp.n_fin) {
       const int64_t nb = (mp.c.n_tiles + 127) / 128;   // ~128 partials (128 KB) per workgroup
       mp.fin_blocks = int(nb < 1 ? 1 : (nb > kPartsBlocksMax ? kPartsBlocksMax : nb));
@@ -3075,11 +3314,27 @@ int32_t slg_triangulate(const slg_maps* maps, const slg_calib* calib, const slg_
   return launch_main3(pick_main<0>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode), m3, tp, out, s);
 }
 
+// One-view fused launches count their own Otsu histograms (main3 SOLO: no stats launch before
+// them); SLG_SOLO=0 restores the stats + fused pair.
+static bool solo_enabled() {
+  static const bool on = [] { const char* e = getenv("SLG_SOLO"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 static int reconstruct_impl(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,
                             const slg_tri_params* tp, void* workspace, const slg_cloud* out, void* stream,
                             bool with_stats) {
   if (!cap || !dp || !workspace) return fail(SLG_ERR_INVALID, "NULL argument");
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (with_stats && dp->thresh_mode == SLG_THRESH_OTSU && solo_enabled() && !(debug_flags() & kMainDbgBits)) {
+    int rc = check_batch(cap, 1);
+    if (rc) return rc;
+    if (cap->n_frames < 4)
+      return fail(SLG_ERR_NOT_ENOUGH, "Not enough images (got %d, need at least 4).", cap->n_frames);
+    if (!tp) return fail(SLG_ERR_INVALID, "NULL argument");
+    return fused_batch(cap, 1, dp, calib, tp, static_cast<char*>(workspace), 0, out, nullptr, s, nullptr, 0,
+                       nullptr, 0, true);
+  }
   if (with_stats) {
     int rc = check_batch(cap, 1);
     if (!rc) rc = make_plan(cap, dp, nullptr);

@@ -270,7 +270,7 @@ def _gray_mode(hv: HostView) -> bool:
     return (hv.kind == "gray" and hv.texture is None) or (hv.kind == "png_z" and hv.channels == 1)
 
 
-def upload_views(hvs, stream) -> list:
+def upload_views(hvs, stream, marks=None) -> list:
     """Async H2D of HostViews on ``stream`` (pinned sources) + the device textures: none for
     gray captures (GRAY mode: the kernels take frame 0), frame 0's BGR for colour ones
     (``slg_rgb_to_gray``).  The PNG captures (kind "png_z") of the list are decoded by ONE
@@ -287,7 +287,7 @@ def upload_views(hvs, stream) -> list:
         devs = [E.DeviceFrames.allocate(hv.n_files, hv.height, hv.width, gray=_gray_mode(hv)) for hv in hvs]
         pngs = [(hv, dev) for hv, dev in zip(hvs, devs) if hv.kind == "png_z"]
         if pngs:
-            decode_png_device(pngs, stream)
+            decode_png_device(pngs, stream, marks)
         for hv, dev in zip(hvs, devs):
             if hv.kind == "gray":
                 dev.data[: hv.n_files].copy_(hv.stack, non_blocking=True)
@@ -308,7 +308,7 @@ def upload_view(hv: HostView, stream) -> E.DeviceFrames:
     return upload_views([hv], stream)[0]
 
 
-def decode_png_device(pngs, stream) -> None:
+def decode_png_device(pngs, stream, marks=None) -> None:
     """Device half of the PNG decode for [(HostView "png_z", DeviceFrames)]: H2D of the zlib
     streams, inflate + un-filter on the GPU (``slg_png_decode_device``, one launch for every
     frame of every view) straight into the frame stacks (gray) or into RGB(A) staging stacks that
@@ -338,10 +338,18 @@ def decode_png_device(pngs, stream) -> None:
         dev._png_keep = (zdev, raw, rgb)                 # alive until the view is collected
         keep.append((hv, dev, rgb))
         k0 += n
+    # the descriptors go up from pageable memory (a small staged copy): pinning them here
+    # allocated page-locked memory on every call
     dbytes = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(descs), ctypes.sizeof(descs))),
-                              dtype=torch.uint8).pin_memory()
+                              dtype=torch.uint8)
     ddev = dbytes.to(device, non_blocking=True)
+    if marks is not None:
+        marks.append(torch.cuda.Event(enable_timing=True))
+        marks[-1].record(stream)
     N.check(L.slg_png_decode_device(ctypes.c_void_p(ddev.data_ptr()), n_all, ctypes.c_void_p(status.data_ptr()), sp))
+    if marks is not None:
+        marks.append(torch.cuda.Event(enable_timing=True))
+        marks[-1].record(stream)
     for hv, dev, rgb in keep:
         if rgb is None:
             pass                                         # gray: GRAY texture mode (frame 0)
@@ -406,6 +414,8 @@ class PipelineStats:
         self.read_s = 0.0             # host: file read + decode (or zstream read) into pinned memory
         self.write_s = 0.0            # host: PLY files written
         self.device_decode_ms = 0.0   # GPU: H2D of the zlib streams + inflate + un-filter
+        self.device_kernels_ms = 0.0  # GPU: the inflate + un-filter launches alone
+        self.device_enqueue_s = 0.0   # host: issuing the device group's uploads and launches
         self.gpu_ms = 0.0             # GPU: reconstruct launches (stats + fused) of every group
         self.folders_host = 0
         self.folders_device = 0
@@ -418,6 +428,8 @@ class PipelineStats:
     def as_dict(self) -> dict:
         return {"wall_s": round(self.wall_s, 4), "read_busy_s": round(self.read_s, 4),
                 "write_busy_s": round(self.write_s, 4), "device_decode_ms": round(self.device_decode_ms, 3),
+                "device_kernels_ms": round(self.device_kernels_ms, 3),
+                "device_enqueue_ms": round(self.device_enqueue_s * 1e3, 2),
                 "gpu_reconstruct_ms": round(self.gpu_ms, 3), "folders_host_decoded": self.folders_host,
                 "folders_device_decoded": self.folders_device}
 
@@ -463,10 +475,14 @@ class BatchPipeline:
         key = (h, w)
         if key not in self.engines:
             n = self._max_views
-            beng = E.BatchReconstructor(h, w, n, slots=2)
-            clouds = [[E.Cloud(h * w, self.row_mode, True) for _ in range(n)] for _ in range(2)]
-            self.engines[key] = (beng, clouds)
-            self.tables[key] = E.DeviceCalib(self.calib, h, w)
+            # made on the compute stream: the default stream shares a hardware queue with the
+            # device-decode stream (tools/queue_probe.py, profiles/r5j), whose inflate launch
+            # would hold these uploads ~225 ms
+            with torch.cuda.stream(self.compute_stream):
+                beng = E.BatchReconstructor(h, w, n, slots=2)
+                clouds = [[E.Cloud(h * w, self.row_mode, True) for _ in range(n)] for _ in range(2)]
+                self.engines[key] = (beng, clouds)
+                self.tables[key] = E.DeviceCalib(self.calib, h, w)
         return self.engines[key], self.tables[key]
 
     def _read(self, folder, device_png: bool) -> HostView:
@@ -479,13 +495,13 @@ class BatchPipeline:
         return hv
 
     # ---- stages
-    def _upload(self, g: _Group, got, stream):
+    def _upload(self, g: _Group, got, stream, marks=None):
         """g.views += the uploads of ``got`` [(entry index, HostView)] on ``stream``: one upload
         (one PNG decode launch) for all of them, or -- when that raises -- view by view, with the
         device decoder's views read again for the host decoder, so a failure stays with its
         folder."""
         try:
-            devs = upload_views([hv for _, hv in got], stream) if got else []
+            devs = upload_views([hv for _, hv in got], stream, marks) if got else []
             g.views += [(k, hv, d) for (k, hv), d in zip(got, devs)]
         except Exception:  # noqa: BLE001
             # what the failed attempt queued (H2D from the pinned stacks, decode launches) must
@@ -519,11 +535,14 @@ class BatchPipeline:
     def _start_device_group(self, g: _Group):
         """Upload + inflate the device group's zlib streams now, on the decode stream."""
         got = self._results(g)
+        t = time.perf_counter()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record(self.decode_stream)
-        self._upload(g, got, self.decode_stream)
+        g.marks = []
+        self._upload(g, got, self.decode_stream, g.marks)
         ev1.record(self.decode_stream)
         g.uploaded = (ev0, ev1)
+        self.stats.add("device_enqueue_s", time.perf_counter() - t)
 
     def _launch(self, g: _Group):
         """Upload g's views (copy stream; done already for the device group) and launch their
@@ -568,8 +587,11 @@ class BatchPipeline:
         self.stats.add("gpu_ms", g.gpu_events[0].elapsed_time(g.gpu_events[1]))
         if g.uploaded is not None:
             self.stats.add("device_decode_ms", g.uploaded[0].elapsed_time(g.uploaded[1]))
+            if len(getattr(g, "marks", ())) == 2:         # the inflate + un-filter launches alone
+                self.stats.add("device_kernels_ms", g.marks[0].elapsed_time(g.marks[1]))
         from .processing import reconstruct_view
-        redo = {k for k, _, dev in g.views if png_failed(dev)}
+        with torch.cuda.stream(self.format_stream):
+            redo = {k for k, _, dev in g.views if png_failed(dev)}
         for k, hv, dev in g.views:               # a frame the device decoder refused: the host decodes
             if k in redo:                        # the whole view again (general path) and runs it alone
                 try:
@@ -585,17 +607,21 @@ class BatchPipeline:
                 except Exception as e:  # noqa: BLE001
                     res[k] = e
         if g.batch is not None:
-            for (k, hv, _), c in zip(g.views, g.clouds):
-                if k in redo:
-                    continue
-                n = int(c.count.item())
-                body = self.formatter.body(c.xyz[:n], c.bgr[:n], self.format_stream) if self.device_ply else None
-                if body is None:                        # host formatting (or a value it must print)
-                    res[k] = (c.xyz[:n].cpu().numpy(), c.bgr[:n].cpu().numpy())
-                else:                                   # the PLY body leaves HBM as bytes
-                    host = self.pool.get((body.numel() + (16 << 20) - 1) // (16 << 20) * (16 << 20))
-                    host[: body.numel()].copy_(body)
-                    res[k] = FormattedCloud(n, host, body.numel(), self.pool)
+            # the reads and copies go on the format stream, not the default one: a stream that
+            # shares its hardware queue with the device-decode stream (4 queues per process)
+            # would hold them behind a ~225 ms inflate launch
+            with torch.cuda.stream(self.format_stream):
+                for (k, hv, _), c in zip(g.views, g.clouds):
+                    if k in redo:
+                        continue
+                    n = int(c.count.item())
+                    body = self.formatter.body(c.xyz[:n], c.bgr[:n], self.format_stream) if self.device_ply else None
+                    if body is None:                    # host formatting (or a value it must print)
+                        res[k] = (c.xyz[:n].cpu().numpy(), c.bgr[:n].cpu().numpy())
+                    else:                               # the PLY body leaves HBM as bytes
+                        host = self.pool.get((body.numel() + (16 << 20) - 1) // (16 << 20) * (16 << 20))
+                        host[: body.numel()].copy_(body)
+                        res[k] = FormattedCloud(n, host, body.numel(), self.pool)
         else:                                       # isolate the failing view(s)
             for k, hv, dev in g.views:
                 if k in redo:
@@ -666,9 +692,13 @@ class BatchPipeline:
                     cur, n_img = [], 0
             if cur:
                 groups.append(cur)
-            prefetch(self.depth)
             if dev_group is not None:
+                # the device group's zlib streams are read and its inflate launch enqueued before
+                # the host decoders take the CPUs (behind them, the enqueue itself waited ~200 ms
+                # and the launch with it: profiles/r5h); two host folders start meanwhile
+                prefetch(2)
                 self._start_device_group(dev_group)
+            prefetch(self.depth)
             done_imgs = 0
             prev = None
             todo = list(groups)                    # host groups as entry lists (made when reached)

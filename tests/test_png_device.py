@@ -202,8 +202,8 @@ def test_pipeline_falls_back_to_host_for_a_refused_frame(tmp_path, N, monkeypatc
     real = PL.decode_png_device
     refused = []
 
-    def refuse_v1(pngs, stream):                     # as if frame 0 of v1 failed its Adler-32 check
-        real(pngs, stream)
+    def refuse_v1(pngs, stream, *a, **k):           # as if frame 0 of v1 failed its Adler-32 check
+        real(pngs, stream, *a, **k)
         for hv, dev in pngs:
             if hv.folder.endswith("v1"):
                 dev._png_status[0] = N.PNG_E_ADLER
@@ -242,8 +242,8 @@ def test_pipeline_group_upload_failure_falls_back_per_view(tmp_path, N, monkeypa
     real = PL.decode_png_device
     failed = []
 
-    def fail_after_queueing(pngs, stream):
-        real(pngs, stream)                           # the inflate launch is queued ...
+    def fail_after_queueing(pngs, stream, *a, **k):
+        real(pngs, stream, *a, **k)                  # the inflate launch is queued ...
         failed.append(len(pngs))
         raise RuntimeError("injected mid-group failure")   # ... and the group upload raises
 
