@@ -278,6 +278,7 @@ class Reconstructor:
         nbytes = int(N.lib().slg_workspace_bytes(self.n_px))
         self.workspace = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         N.check(N.lib().slg_workspace_init(_vp(self.workspace), nbytes, _stream()))
+        torch.cuda.current_stream(self.device).synchronize()     # (as BatchReconstructor)
 
     def _check_geometry(self, h, w):
         if (h, w) != (self.height, self.width):
@@ -408,6 +409,9 @@ class BatchReconstructor:
         for v in range(self.max_views * self.slots):
             N.check(N.lib().slg_workspace_init(ctypes.c_void_p(self.workspace.data_ptr() + v * self.ws_stride),
                                                self.ws_stride, _stream()))
+        # the slices are zeroed on the current stream; launches may come on any other (pool
+        # streams do not wait for it): done before the constructor returns
+        torch.cuda.current_stream(self.device).synchronize()
         self._events = []
 
     def _ws(self, slot: int) -> ctypes.c_void_p:
@@ -586,6 +590,12 @@ class BatchReconstructor:
         stop = n if stop is None else min(int(stop), n)
         if not 0 <= start <= stop:
             raise ValueError("bad start/stop")
+        if start == 0 and isinstance(main_stream, torch.cuda.Stream):
+            # the frames, tables and clouds the caller made on its current stream come first
+            cur = torch.cuda.current_stream(main_stream.device)
+            for st in (main_stream, stats_stream):
+                if isinstance(st, torch.cuda.Stream) and st != cur:
+                    st.wait_stream(cur)
         for k in range(1, n):
             if batches[k].slot == batches[k - 1].slot:
                 raise ValueError("consecutive batches must use different workspace slots")

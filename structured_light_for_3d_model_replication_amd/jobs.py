@@ -146,6 +146,7 @@ class ResidentJob:
         on the two streams); afterwards ``s0`` has joined ``s1``.  No host sync.  Forgets any
         earlier :meth:`recover`."""
         self._recovered.clear()
+        s0.wait_stream(torch.cuda.current_stream(self.device))   # the staged views, tables, arena
         s1.wait_stream(s0)
         self.engine.run_pipelined(self.batches, s0, s1, mode="fused2")
         s0.wait_stream(s1)
