@@ -181,6 +181,23 @@ constexpr int kStatsBlocksSolo = SLG_STATS_BLOCKS_SOLO;   // one-view launches (
 #define SLG_OTSU_SOLO_CHUNKS 2
 #endif
 constexpr int kOtsuSoloChunks = SLG_OTSU_SOLO_CHUNKS;
+// SLG_SOLO_PROF=1 (A/B builds only, tools/solo_prof.py): per-workgroup s_memrealtime stamps of a
+// one-view fused launch -- [0] start, [1] stats done, [2] frame loads issued, [3] thresholds
+// seen, [4] phase A done, [5] exit; the finisher adds [6] Otsu start, [7] flag raised.
+#ifndef SLG_SOLO_PROF
+#define SLG_SOLO_PROF 0
+#endif
+#if SLG_SOLO_PROF
+__device__ uint64_t g_solo_rec[1024 * 8];
+#define SOLO_STAMP(k)                                                                  \
+  do {                                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_solo_rec[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define SOLO_STAMP(k) \
+  do {            \
+  } while (0)
+#endif
 
 struct StatsParams {
   const uint8_t* white[kMaxBatch];
@@ -348,7 +365,11 @@ __device__ __attribute__((always_inline)) inline void mu1_chain_lds(int lo, int 
   }
 }
 
+#ifndef SLG_OTSU_PRIO
+#define SLG_OTSU_PRIO 0     // s_setprio of the Otsu waves (the chains are issue-bound), 0: none
+#endif
 __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t* h, int64_t n, double* lds) {
+  if (SLG_OTSU_PRIO) __builtin_amdgcn_s_setprio(SLG_OTSU_PRIO);
   SLG_OTSU_MARK(0);
   const int lane = threadIdx.x & 63;
   const double scale = 1.0 / double(n);
@@ -564,6 +585,7 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
     if (ob > best || (ob == best && oi < best_i)) { best = ob; best_i = oi; }
   }
   SLG_OTSU_MARK(7);
+  if (SLG_OTSU_PRIO) __builtin_amdgcn_s_setprio(0);
   return best_i == INT_MAX ? 0.0 : double(best_i);
 }
 
@@ -1152,8 +1174,10 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
       // microsecond on the memory system: 170 us per one-view launch, profiles/r5l)
       // what the thresholds' workgroup wrote and the waves read next -- smin, cmin, the zeroed
       // look-back words -- is read by agent-scope atomics, so no cache invalidation is needed
+      SOLO_STAMP(2);
       if (threadIdx.x == 0) solo_wait(p.ws);
       __syncthreads();
+      SOLO_STAMP(3);
       smin = __hip_atomic_load(&p.ws->smin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       cmin = __hip_atomic_load(&p.ws->cmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       pre(w);                                       // (a gray capture's colour: the white bytes)
@@ -1941,6 +1965,8 @@ __device__ __attribute__((always_inline)) inline void solo_stats(const MainParam
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   WsHeader* ws = p.ws;
   uint32_t* hist_part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + kHistPartOff);
+  // (claiming the next chunk while counting this one made a few workgroups take two chunks
+  // each and the last ticket come later: 34 vs 25 us, profiles/r5o)
   for (;;) {
     if (tid == 0) *s_flag = int(atomicAdd(&ws->solo[0], 1u));
     __syncthreads();
@@ -1970,6 +1996,7 @@ __device__ __attribute__((always_inline)) inline void solo_stats(const MainParam
     }
     __syncthreads();
     if (*s_flag) {                                   // the last chunk: thresholds for the launch
+      SOLO_STAMP(6);
       if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       __syncthreads();
       uint32_t* hg = s_lds;
@@ -1996,17 +2023,21 @@ __device__ __attribute__((always_inline)) inline void solo_stats(const MainParam
           }
           ws->above[wave] = above;
         }
+      } else {                                       // the other waves meanwhile: arm the look-back,
+        static_assert(kTileBlock > 128, "the resets need waves beside the two Otsu waves");
+        const int t = tid - 128;                     // reset the histogram copies
+        uint64_t* states = p.states;
+        for (int64_t i = t; i < n_state_words; i += kTileBlock - 128) states[i] = 0;
+        for (int i = t; i < kHistCopies * 512; i += kTileBlock - 128) hist_part[i] = 0;
+        if (t == 0) { ws->solo[1] = 0; ws->tile_counter = 0; }
       }
-      uint64_t* states = p.states;
-      for (int64_t i = tid; i < n_state_words; i += kTileBlock) states[i] = 0;   // arm the look-back
-      for (int i = tid; i < kHistCopies * 512; i += kTileBlock) hist_part[i] = 0;
-      if (tid == 0) { ws->solo[1] = 0; ws->tile_counter = 0; }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_store(&ws->solo[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      SOLO_STAMP(7);
     }
     __syncthreads();
   }
@@ -2078,8 +2109,14 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // look-back, D stores (100 MHz ticks), look-back polls, sleep units, items, start} written to
   // view 0's partials region (tools/kbench.py "phases"; the host refuses it when a batch is
   // carried, whose partials live there).
-  if constexpr (SOLO)                                // the view's thresholds, counted right here
+  if constexpr (SOLO) {                              // the view's thresholds, counted right here
+    SOLO_STAMP(0);
+#if SLG_SOLO_PROF
+    if (tid == 0 && blockIdx.x < 1024) { g_solo_rec[blockIdx.x * 8 + 6] = 0; g_solo_rec[blockIdx.x * 8 + 7] = 0; }
+#endif
     solo_stats(p, tiles, P.n_state_words, P.pad_zero, s_hstage, s_hn, reinterpret_cast<uint32_t*>(s_item), &s_wtot[0]);
+    SOLO_STAMP(1);
+  }
   const bool prof = PROF && (p.dbg & 64) != 0;
   uint64_t t_phase = prof ? __builtin_amdgcn_s_memrealtime() : 0;
   // the record lives in LDS (tid 0 writes it): as a register array it pushed the profiling
@@ -2178,6 +2215,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     }
   }
   __syncthreads();
+  if constexpr (SOLO) SOLO_STAMP(4);
   if (SLG_PRIO_A) __builtin_amdgcn_s_setprio(0);
   if (SLG_WB_PREFETCH > 0 && (pf_a ^ pf_b) == 0x9e3779b9u && p.dbg == 0x7fffffff)
     atomicOr(&p.ws->error, 0u);                      // (never: keeps the prefetch loads)
@@ -2455,7 +2493,10 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       if (!(PROF && (p.dbg & 8)))
         bgr_tile_store(s == 0 ? p.bgr : p.scratch_bgr, int64_t(s_excl[s]), s_agg[s], s_stage + s * kStageWords);
   }
-  if constexpr (SOLO) solo_exit(p.ws, int(gridDim.x));
+  if constexpr (SOLO) {
+    solo_exit(p.ws, int(gridDim.x));
+    SOLO_STAMP(5);
+  }
   if (prof) {
     __syncthreads();
     stamp(3);
@@ -3314,11 +3355,19 @@ int32_t slg_triangulate(const slg_maps* maps, const slg_calib* calib, const slg_
   return launch_main3(pick_main<0>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode), m3, tp, out, s);
 }
 
-// One-view fused launches count their own Otsu histograms (main3 SOLO: no stats launch before
-// them); SLG_SOLO=0 restores the stats + fused pair.
+#if SLG_SOLO_PROF
+extern "C" int32_t slg_solo_prof_read(void* host, int64_t n_words) {   // (A/B builds only)
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_solo_rec), size_t(n_words) * 8) == hipSuccess ? 0 : 2;
+}
+#endif
+
+// One-view fused launches that count their own Otsu histograms (main3 SOLO: no stats launch
+// before them) with SLG_SOLO=1.  Off by default: 93.5 vs 60.8 us per one-view call, the last
+// chunk's ticket lands ~34 us in (its loads queue behind the other workgroups' frame reads) and
+// the finisher's Otsu takes ~24 us beside them (12.7 alone): tools/solo_prof.py, profiles/r5o.
 static bool solo_enabled() {
-  static const bool on = [] { const char* e = getenv("SLG_SOLO"); return !(e && e[0] == '0'); }();
-  return on;
+  const char* e = getenv("SLG_SOLO");               // (read per call: tests switch it)
+  return e && e[0] == '1';
 }
 
 static int reconstruct_impl(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,

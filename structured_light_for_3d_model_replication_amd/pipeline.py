@@ -33,6 +33,7 @@ import ctypes
 import os
 import threading
 import time
+from collections import deque
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 
@@ -420,6 +421,23 @@ class PipelineStats:
         self.folders_host = 0
         self.folders_device = 0
         self.wall_s = 0.0
+        # SLG_PIPE_TRACE=1: a timeline of (stage, thread, start_s, end_s, what) from the run's
+        # start -- host spans from perf_counter, GPU spans from HIP events (tools/e2e_files.py)
+        self.trace = [] if os.environ.get("SLG_PIPE_TRACE") else None
+        self.t0 = time.perf_counter()
+        self.ev0 = None
+
+    def span(self, name: str, t0: float, t1: float, what: str = ""):
+        if self.trace is not None:
+            with self._lock:
+                self.trace.append((name, threading.current_thread().name, round(t0 - self.t0, 5),
+                                   round(t1 - self.t0, 5), what))
+
+    def gpu_span(self, name: str, a, b, what: str = ""):
+        """A GPU span between two completed timing events (recorded after ``ev0``)."""
+        if self.trace is not None and self.ev0 is not None:
+            t0 = self.ev0[1] + self.ev0[0].elapsed_time(a) * 1e-3
+            self.span(name, t0, t0 + a.elapsed_time(b) * 1e-3, what)
 
     def add(self, key: str, v: float):
         with self._lock:
@@ -490,7 +508,9 @@ class BatchPipeline:
         try:
             hv = read_view(folder, self.cfg, self.pool, self.order, device_png=device_png)
         finally:
-            self.stats.add("read_s", time.perf_counter() - t)
+            t1 = time.perf_counter()
+            self.stats.add("read_s", t1 - t)
+            self.stats.span("read_z" if device_png else "read", t, t1, os.path.basename(folder))
         self.stats.add("folders_device" if hv.kind == "png_z" else "folders_host", 1)
         return hv
 
@@ -542,13 +562,18 @@ class BatchPipeline:
         self._upload(g, got, self.decode_stream, g.marks)
         ev1.record(self.decode_stream)
         g.uploaded = (ev0, ev1)
-        self.stats.add("device_enqueue_s", time.perf_counter() - t)
+        t1 = time.perf_counter()
+        self.stats.add("device_enqueue_s", t1 - t)
+        self.stats.span("device_enqueue", t, t1)
 
     def _launch(self, g: _Group):
         """Upload g's views (copy stream; done already for the device group) and launch their
         reconstruction (compute stream)."""
+        t = time.perf_counter()
         if g.uploaded is None:
-            self._upload(g, self._results(g), self.copy_stream)
+            got = self._results(g)
+            self.stats.span("wait_reads", t, time.perf_counter())
+            self._upload(g, got, self.copy_stream)
         if not g.views:
             return
         if g.uploaded is not None:
@@ -577,18 +602,25 @@ class BatchPipeline:
         g.gpu_events = (g0, g1)
         g.event = torch.cuda.Event()
         g.event.record(self.compute_stream)
+        self.stats.span("launch", t, time.perf_counter(), f"{len(g.views)} views")
 
     def _collect(self, g: _Group):
         """Results of g's views as host (P float64 [N,3], C uint8 [N,3]) or exceptions."""
         res = {}
         if not g.views:
             return res
+        t = time.perf_counter()
         g.event.synchronize()
+        t_sync = time.perf_counter()
+        self.stats.span("wait_gpu", t, t_sync)
         self.stats.add("gpu_ms", g.gpu_events[0].elapsed_time(g.gpu_events[1]))
+        self.stats.gpu_span("gpu_reconstruct", *g.gpu_events, f"{len(g.views)} views")
         if g.uploaded is not None:
             self.stats.add("device_decode_ms", g.uploaded[0].elapsed_time(g.uploaded[1]))
+            self.stats.gpu_span("gpu_device_decode", *g.uploaded)
             if len(getattr(g, "marks", ())) == 2:         # the inflate + un-filter launches alone
                 self.stats.add("device_kernels_ms", g.marks[0].elapsed_time(g.marks[1]))
+                self.stats.gpu_span("gpu_inflate", *g.marks)
         from .processing import reconstruct_view
         with torch.cuda.stream(self.format_stream):
             redo = {k for k, _, dev in g.views if png_failed(dev)}
@@ -602,8 +634,8 @@ class BatchPipeline:
                         (_, _), dc = self._engine(dev2.height, dev2.width)
                         res[k] = reconstruct_view(dev2, self.cfg, self.calib, self.row_mode, self.tol, dc=dc)
                     finally:
-                        for t in hv2.pinned:
-                            self.pool.put(t)
+                        for b in hv2.pinned:
+                            self.pool.put(b)
                 except Exception as e:  # noqa: BLE001
                     res[k] = e
         if g.batch is not None:
@@ -632,8 +664,9 @@ class BatchPipeline:
                 except Exception as e:  # noqa: BLE001
                     res[k] = e
         for _, hv, _ in g.views:                    # uploads are complete: recycle the host buffers
-            for t in hv.pinned:
-                self.pool.put(t)
+            for b in hv.pinned:
+                self.pool.put(b)
+        self.stats.span("format_d2h", t_sync, time.perf_counter(), f"{len(g.views)} views")
         return res
 
     def run(self, subfolders, write) -> int:
@@ -642,6 +675,11 @@ class BatchPipeline:
         from .processing import has_images
         t_run = time.perf_counter()
         self.stats = LAST_STATS = PipelineStats()
+        if self.stats.trace is not None:             # the GPU spans' time base
+            self.stats.ev0 = (torch.cuda.Event(enable_timing=True), 0.0)
+            torch.cuda.synchronize()
+            self.stats.ev0[0].record(self.compute_stream)
+            self.stats.ev0 = (self.stats.ev0[0], time.perf_counter())
         entries = [(f, has_images(f)) for f in subfolders]
         success = 0
         order = [f for f, ok in entries if ok]
@@ -664,15 +702,32 @@ class BatchPipeline:
             try:
                 return write(folder, result)
             finally:
-                self.stats.add("write_s", time.perf_counter() - t)
+                t1 = time.perf_counter()
+                self.stats.add("write_s", t1 - t)
+                self.stats.span("write", t, t1, os.path.basename(folder))
 
+        # the device group's zlib-stream reads (file read + CRCs, no inflate) on a pool of their
+        # own, so they do not queue behind the host decoders' folders (or these behind them)
+        zpool = ThreadPoolExecutor(max_workers=4) if n_dev else None
+        try:
+            success = self._run_groups(entries, order, mode, n_dev, cut, zpool, timed_write)
+        finally:
+            if zpool is not None:
+                zpool.shutdown()
+        self.stats.wall_s = time.perf_counter() - t_run
+        return success
+
+    def _run_groups(self, entries, order, mode, n_dev, cut, zpool, timed_write) -> int:
+        """The group loop of :meth:`run` (reads, device group, launches, collects, writes)."""
+        success = 0
+        dev_first = len(order) - n_dev
         with ThreadPoolExecutor(max_workers=2) as reader, ThreadPoolExecutor(max_workers=self.writers) as writer:
             futs = {}
             all_dev = mode == "all"
             dev_group = None
             if n_dev:                                # the device group's zlib streams first: its
                 ents = entries[cut:]                 # launch starts while the host decodes the rest
-                dev_group = _Group([(f, reader.submit(self._read, f, True) if ok else None) for f, ok in ents])
+                dev_group = _Group([(f, zpool.submit(self._read, f, True) if ok else None) for f, ok in ents])
             host_order = order[:dev_first]
             nxt = 0
 
@@ -693,10 +748,10 @@ class BatchPipeline:
             if cur:
                 groups.append(cur)
             if dev_group is not None:
-                # the device group's zlib streams are read and its inflate launch enqueued before
-                # the host decoders take the CPUs (behind them, the enqueue itself waited ~200 ms
-                # and the launch with it: profiles/r5h); two host folders start meanwhile
-                prefetch(2)
+                # the inflate launch is enqueued as soon as the device group's streams are read;
+                # the host decoders start meanwhile (SLG_PIPE_HOST_FIRST folders of them, default
+                # the whole read-ahead: two reader threads at most, so the z reads keep CPUs)
+                prefetch(int(os.environ.get("SLG_PIPE_HOST_FIRST", self.depth)))
                 self._start_device_group(dev_group)
             prefetch(self.depth)
             done_imgs = 0
@@ -704,6 +759,22 @@ class BatchPipeline:
             todo = list(groups)                    # host groups as entry lists (made when reached)
             if dev_group is not None:
                 todo.append(dev_group)
+            # groups whose PLYs are being written: their log lines go out in folder order once
+            # their writes are done; the loop blocks on the oldest only past `max_writing` views
+            # (blocking on every group serialised its writes with the next group's collect:
+            # ~10 ms per C2 view, profiles/r5n)
+            writing: deque = deque()
+            max_writing = max(2 * self.writers, self.group)
+
+            def flush(block_until: int):
+                nonlocal success
+                t = time.perf_counter()
+                while writing and (sum(len(o) for _, o in writing) > block_until
+                                   or all(wf is None or wf.done() for _, wf, _ in writing[0][1].values())):
+                    success += self._log_group(*writing.popleft())
+                if time.perf_counter() - t > 1e-4:
+                    self.stats.span("report_wait", t, time.perf_counter())
+
             for gi, item in enumerate(todo + [None]):
                 g = None
                 if isinstance(item, _Group):
@@ -716,18 +787,18 @@ class BatchPipeline:
                     res = self._collect(prev)
                     done_imgs += sum(1 for _, fut in prev.entries if fut is not None)
                     prefetch(done_imgs + self.depth)
-                    success += self._report(prev, res, timed_write, writer)
+                    writing.append((prev, self._submit_writes(prev, res, timed_write, writer)))
+                    flush(max_writing)
                 prev = g
-        self.stats.wall_s = time.perf_counter() - t_run
+            flush(-1)
         return success
 
-    def _report(self, g: _Group, res, write, writer) -> int:
-        """The group's PLYs written (writer thread, in order) and its log lines in exactly the
-        reference's order per folder: Decoding, then Reconstructing / Saving / ✔ Saved, or the
-        ❌ Error line.  Returns the folders that succeeded."""
-        log, ok, cfg = self.log, 0, self.cfg
+    @staticmethod
+    def _submit_writes(g: _Group, res, write, writer) -> dict:
+        """Start the group's PLY writes (writer threads): entry index -> (result, write future
+        or None, error)."""
         outcome = {}
-        for k, (folder, fut) in enumerate(g.entries):          # start every write first
+        for k, (folder, fut) in enumerate(g.entries):
             if fut is None:
                 continue
             err = g.errors.get(k)
@@ -735,6 +806,13 @@ class BatchPipeline:
             if err is None and isinstance(r, Exception):
                 err = r
             outcome[k] = (r, None if err is not None else writer.submit(write, folder, r), err)
+        return outcome
+
+    def _log_group(self, g: _Group, outcome: dict) -> int:
+        """The group's log lines (after its writes) in exactly the reference's order per folder:
+        Decoding, then Reconstructing / Saving / ✔ Saved, or the ❌ Error line.  Returns the
+        folders that succeeded."""
+        log, ok, cfg = self.log, 0, self.cfg
         for k, (folder, fut) in enumerate(g.entries):
             name = os.path.basename(folder)
             if fut is None:

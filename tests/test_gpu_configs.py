@@ -295,3 +295,27 @@ def test_valid_bounds_match_histogram_counts(mods, scan):
         want = min(int(np.count_nonzero(w > ts)), int(np.count_nonzero((w - b) > tc)))
         assert g == want
         assert g >= int(np.count_nonzero(O.mask_processing(v.frames[0], v.frames[1])))
+
+
+@pytest.mark.parametrize("x64", [False, True])
+def test_one_view_solo_launch_matches_pair(mods, scan, monkeypatch, x64):
+    """SLG_SOLO=1 (opt-in): the one-view fused launch that counts its own Otsu histograms gives
+    the stats + fused pair's clouds bit for bit (counts, XYZ, BGR) on 6 full-size C2 views, the
+    oracle's point counts, and raises no SOLO error flag (bit 2)."""
+    E, N = mods
+    import torch
+    cal, views = scan
+    cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
+    dcal = E.DeviceCalib(cal, 1080, 1920)
+    eng = E.Reconstructor(1080, 1920)
+    want = _oracle_all(cal, views[:6], (11, 10))
+    for v, (wp, _) in zip(views[:6], want):
+        d = E.DeviceFrames(list(v.frames), v.texture)
+        monkeypatch.setenv("SLG_SOLO", "0")
+        P0, C0 = (t.clone() for t in eng.reconstruct(d, cfg, dcal, 1, xyz_f64=x64).result())
+        monkeypatch.setenv("SLG_SOLO", "1")
+        for _ in range(2):                               # the launch re-arms its own words
+            P1, C1 = eng.reconstruct(d, cfg, dcal, 1, xyz_f64=x64).result()
+            assert eng.error_flags() & 4 == 0
+            assert len(P1) == len(wp)
+            assert torch.equal(P0, P1) and torch.equal(C0, C1)

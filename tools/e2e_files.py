@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--reps", type=int, default=1, help="repetitions of the whole list (interleaved)")
     ap.add_argument("--parts", action="store_true", help="also the serial per-stage costs")
     ap.add_argument("--out", default="", help="also write the JSON here")
+    ap.add_argument("--trace", default="", help="write each run's pipeline timeline (SLG_PIPE_TRACE) here")
     args = ap.parse_args()
 
     from structured_light_for_3d_model_replication_amd import calibration, synth
@@ -62,7 +63,9 @@ def main():
         kw = dict(n_sets_col=11, n_sets_row=10)
         PR.ProcessingLogic.process_multi_ply(calib, folders[0], "single", log_callback=lambda m: None, **kw)  # warm-up
         runs = [(r.split(":") + [""])[:3] for r in args.runs.split(",") if r]
-        res, plys = {}, {}
+        res, plys, traces = {}, {}, {}
+        if args.trace:
+            os.environ["SLG_PIPE_TRACE"] = "1"
         env = {"host": "0", "auto": "auto", "device": "1"}
         for rep in range(args.reps):
             for dec, g, extra in runs:
@@ -84,6 +87,8 @@ def main():
                 key = f"{dec}_group{g}" + (f"_{extra}" if extra else "")
                 st = PL.LAST_STATS.as_dict()
                 res.setdefault(key, []).append({"s_per_view": round(dt / args.views, 4), **st})
+                if PL.LAST_STATS.trace is not None:
+                    traces[f"{key}_rep{rep}"] = sorted(PL.LAST_STATS.trace, key=lambda e: e[2])
                 print(f"[e2e] rep {rep} {key}: {dt / args.views:.4f} s/view {st}", file=sys.stderr, flush=True)
                 plys[key] = [open(os.path.join(f, os.path.basename(f) + ".ply"), "rb").read() for f in folders]
         first = next(iter(plys.values()))
@@ -122,6 +127,9 @@ def main():
                 parts[dec] = {"read_pinned": round(t_read / n, 4), "h2d_decode_kernels_d2h": round(t_rec / n, 4),
                               "ply_write": round(t_ply / n, 4)}
             out["s_per_view_parts_serial"] = parts
+        if args.trace:
+            with open(args.trace, "w") as f:
+                json.dump(traces, f)
         line = json.dumps(out)
         print(line, flush=True)
         if args.out:
