@@ -184,6 +184,9 @@ constexpr int kOtsuSoloChunks = SLG_OTSU_SOLO_CHUNKS;
 // SLG_SOLO_PROF=1 (A/B builds only, tools/solo_prof.py): per-workgroup s_memrealtime stamps of a
 // one-view fused launch -- [0] start, [1] stats done, [2] frame loads issued, [3] thresholds
 // seen, [4] phase A done, [5] exit; the finisher adds [6] Otsu start, [7] flag raised.
+#ifndef SLG_STATS_FENCE
+#define SLG_STATS_FENCE 0   // release / acquire fences around the stats tickets (atomics only: unneeded)
+#endif
 #ifndef SLG_SOLO_PROF
 #define SLG_SOLO_PROF 0
 #endif
@@ -803,11 +806,14 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   }
   if (!otsu && tid == 0 && s_maxd) atomicMax(&ws->max_diff_enc, s_maxd);
 
-  // Publish (every wave drains its atomics, barrier, one release) then take a ticket.
+  // Publish (every wave drains its atomics, barrier) then take a ticket.  What the last arriver
+  // reads -- the histogram copies, max_diff_enc -- is written and read by agent-scope atomics
+  // only, performed at the point of coherence once vmcnt says so: no L2 write-back / invalidate
+  // (SLG_STATS_FENCE=1 restores the release / acquire fences).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (SLG_STATS_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t t = __hip_atomic_fetch_add(&ws->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (t == gridDim.x - 1) ? 1u : 0u;
@@ -815,8 +821,8 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   __syncthreads();
   if (!s_last) return;
 
-  // Last arriver: acquire, read the global histograms, compute thresholds, reset for reuse.
-  if (tid == 0) {
+  // Last arriver: read the global histograms, compute thresholds, reset for reuse.
+  if (SLG_STATS_FENCE && tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -906,17 +912,17 @@ __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint
     if (a1) atomicAdd(dst + 1, a1);
   }
 
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (atomics only: see stats_kernel)
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (SLG_STATS_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t t = __hip_atomic_fetch_add(&ws->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *s_last = (t == uint32_t(n_blocks) - 1) ? 1u : 0u;
   }
   __syncthreads();
   if (!*s_last) return;
-  if (tid == 0) {
+  if (SLG_STATS_FENCE && tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }

@@ -113,36 +113,55 @@ def device_png_enabled() -> bool:
     return device_png_mode() == "all"
 
 
-# Host PNG decode on the box's 16 CPUs: ~20 ms per C2 view (profiles/r4o); one device inflate
-# launch: ~225 ms whatever its size, up to 768 streams in flight (17 views of 44 frames).  A batch
-# overlaps the two when the host has about that long of its own work: the last n - 12 folders
-# (at most 16) go to ONE device launch started at the beginning, the host threads decode the
-# rest meanwhile.
-HOST_AHEAD = 12
+# Host PNG decode on the box's 16 CPUs: ~70 C2 views/s with two folders in flight (profiles/r5o,
+# 14 ms per view); one device inflate launch: ~230-400 ms whatever its size (one wave per stream,
+# a serial Huffman chain each; up to 768 streams in flight).  The device pays only when the host
+# has at least that long of its own work, ~26 views: the last n - 26 folders (at most 16) go to
+# ONE device launch started at the beginning, the host threads decode the rest meanwhile
+# (36 folders: 10 device views, 0.0156-0.0160 s/view against 0.0164-0.0166 host-only and
+# 0.0196-0.0234 with 16 device views, profiles/r5p).
+HOST_AHEAD = 26
 DEVICE_MAX_VIEWS = 16
 
 
 _DECODE_STREAMS: dict = {}
+PNG_WAVES_PER_CU = 3        # png_inflate_kernel: one 64-lane wave per stream, ~50 KB of LDS each
 
 
-def png_decode_stream(device: int | None = None):
-    """The device PNG decode's stream, one per GPU for the process: every ``SLG_PNG_RESERVE_EVERY``
-    -th CU (default 16th) left out of its CU mask (``slg_stream_create_reserving``), so the
-    ~225 ms inflate launch leaves 16 of 256 CUs to the fused launches of the host-decoded views
-    (their 72 KB of LDS per workgroup fit on no CU the inflate's 50 KB waves hold); a plain
-    stream when the mask cannot be set.  240 CUs x 3 inflate waves still hold a 16-view group's
-    704 streams at once."""
+def png_reserve_every(n_streams: int | None, n_cus: int) -> int:
+    """Every how-many-th CU the device PNG decode leaves to the other launches: the most CUs
+    (smallest k >= 2) whose complement still holds all ``n_streams`` inflate waves at once
+    (``PNG_WAVES_PER_CU`` each), so the fused launches of the host-decoded views beside it are not
+    squeezed onto a few CUs (16 free CUs made an 8-view group's kernels take ~100 ms instead of
+    ~8: profiles/r5p); 16 when the count is unknown.  SLG_PNG_RESERVE_EVERY overrides."""
+    env = os.environ.get("SLG_PNG_RESERVE_EVERY")
+    if env is not None:
+        return int(env)
+    if not n_streams:
+        return 16
+    for k in range(2, 65):
+        if (n_cus - n_cus // k) * PNG_WAVES_PER_CU >= n_streams:
+            return k
+    return 0                                         # more streams than fit: no CU left out
+
+
+def png_decode_stream(device: int | None = None, n_streams: int | None = None):
+    """The device PNG decode's stream, one per GPU and CU mask for the process: every k-th CU
+    (:func:`png_reserve_every`) left out of its CU mask (``slg_stream_create_reserving``), so the
+    inflate launch -- ~250-400 ms, one wave per stream -- leaves those CUs to the fused launches
+    of the host-decoded views (their 72 KB of LDS per workgroup fit on no CU the inflate's 50 KB
+    waves hold); a plain stream when the mask cannot be set."""
     dev = torch.cuda.current_device() if device is None else int(device)
-    s = _DECODE_STREAMS.get(dev)
+    every = png_reserve_every(n_streams, torch.cuda.get_device_properties(dev).multi_processor_count)
+    s = _DECODE_STREAMS.get((dev, every))
     if s is None:
-        every = int(os.environ.get("SLG_PNG_RESERVE_EVERY", "16"))
         h = ctypes.c_void_p()
         with torch.cuda.device(dev):
             if every >= 2 and N.lib().slg_stream_create_reserving(every, ctypes.byref(h)) == 0:
                 s = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", dev))
             else:
                 s = torch.cuda.Stream(device=dev)
-        _DECODE_STREAMS[dev] = s
+        _DECODE_STREAMS[(dev, every)] = s
     return s
 
 
@@ -480,7 +499,7 @@ class BatchPipeline:
         self.copy_stream = torch.cuda.Stream()
         self.compute_stream = torch.cuda.Stream()
         self.format_stream = torch.cuda.Stream()     # PLY bodies of group k beside group k+1's kernels
-        self.decode_stream = png_decode_stream()     # the device-decoded group's H2D + inflate
+        self.decode_stream = None                    # the device group's H2D + inflate (sized to it)
         self.formatter = PLY.DeviceFormatter()
         self.device_ply = device_ply
         self.engines: dict = {}
@@ -556,6 +575,7 @@ class BatchPipeline:
         """Upload + inflate the device group's zlib streams now, on the decode stream."""
         got = self._results(g)
         t = time.perf_counter()
+        self.decode_stream = png_decode_stream(n_streams=sum(len(hv.z[0]) for _, hv in got if hv.kind == "png_z"))
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record(self.decode_stream)
         g.marks = []
@@ -764,7 +784,7 @@ class BatchPipeline:
             # (blocking on every group serialised its writes with the next group's collect:
             # ~10 ms per C2 view, profiles/r5n)
             writing: deque = deque()
-            max_writing = max(2 * self.writers, self.group)
+            max_writing = max(3 * self.writers, 2 * self.group)
 
             def flush(block_until: int):
                 nonlocal success

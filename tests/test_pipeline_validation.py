@@ -148,3 +148,20 @@ def test_resident_job_damage_reaches_every_overwritten_view():
     assert job.damaged([10, 5, 5, 20, 8]) == [] and job.overflowed([10, 5, 5, 20, 8]) == []
     assert job.overflowed([16, 5, 5, 20, 8]) == [0] and job.damaged([16, 5, 5, 20, 8]) == [0, 1, 2]
     assert job.damaged([10, 5, 6, 20, 9]) == [2, 3, 4]      # 15 + 6 > 20; the last view has no successor
+
+
+def test_png_reserve_every_fits_the_device_group(monkeypatch):
+    """The device PNG decode's CU mask leaves out as many CUs as it can while every inflate wave
+    of the group still fits (3 per CU): 10 C2 views (440 streams) leave every 3rd CU."""
+    from structured_light_for_3d_model_replication_amd import pipeline as PL
+    monkeypatch.delenv("SLG_PNG_RESERVE_EVERY", raising=False)
+    assert PL.png_reserve_every(None, 256) == 16
+    assert PL.png_reserve_every(440, 256) == 3
+    for n in (1, 44, 440, 528, 704, 720):
+        k = PL.png_reserve_every(n, 256)
+        assert (256 - 256 // k) * PL.PNG_WAVES_PER_CU >= n
+        if k > 2:
+            assert (256 - 256 // (k - 1)) * PL.PNG_WAVES_PER_CU < n
+    assert PL.png_reserve_every(800, 256) == 0
+    monkeypatch.setenv("SLG_PNG_RESERVE_EVERY", "8")
+    assert PL.png_reserve_every(44, 256) == 8
