@@ -237,14 +237,17 @@ int32_t slg_png_gray8_size(const char* path, int32_t* width, int32_t* height) {
 // `out` unspecified.  Thread-safe; meant to run on a host decode pool (ctypes drops the GIL).
 int32_t slg_png_gray8_decode(const char* path, uint8_t* out, int64_t cap, int32_t width, int32_t height) {
   if (!path || !out) return kInvalid;
-  std::vector<uint8_t> b;
+  // the file, its zlib stream and the filtered rows in buffers the decode thread keeps: a frame
+  // is ~1 MB + 1 MB + 2 MB, and fresh ones per frame cost page faults and a 2 MB zero fill
+  thread_local std::vector<uint8_t> b, raw;
+  thread_local Png png;
   if (!read_file(path, b)) return kInvalid;
-  Png png;
+  png.idat.clear();
   int rc = parse(b, png, true);
   if (rc) return rc;
   if (int32_t(png.w) != width || int32_t(png.h) != height || cap < int64_t(png.w) * png.h) return kInvalid;
-  std::vector<uint8_t> raw(size_t(png.h) * (png.w + 1));
-  if (!inflate_all(png.idat, raw.data(), raw.size())) return kInvalid;
+  if (raw.size() < size_t(png.h) * (png.w + 1)) raw.resize(size_t(png.h) * (png.w + 1));
+  if (!inflate_all(png.idat, raw.data(), size_t(png.h) * (png.w + 1))) return kInvalid;
   return unfilter(raw.data(), out, png.w, png.h) ? kOk : kInvalid;
 }
 

@@ -14,7 +14,8 @@ from __future__ import annotations
 
 import glob
 import os
-from concurrent.futures import ThreadPoolExecutor
+import threading
+from concurrent.futures import ThreadPoolExecutor, wait
 
 import numpy as np
 
@@ -122,6 +123,31 @@ def decode_threads() -> int:
     except AttributeError:
         n = os.cpu_count() or 8
     return max(1, min(16, n))
+
+
+_POOLS: dict = {}
+_POOLS_LOCK = threading.Lock()
+
+
+def decode_pool() -> ThreadPoolExecutor:
+    """The process's host decode pool (:func:`decode_threads` threads, kept across views): the
+    native decoder keeps its per-thread buffers warm in it, and two folders read at once share
+    the CPUs instead of each starting a pool of its own."""
+    n = decode_threads()
+    with _POOLS_LOCK:
+        ex = _POOLS.get(n)
+        if ex is None:
+            ex = _POOLS[n] = ThreadPoolExecutor(max_workers=n, thread_name_prefix="slg-decode")
+        return ex
+
+
+def decode_all(fn, items) -> list:
+    """``[fn(x) for x in items]`` on :func:`decode_pool`; every call has finished when this
+    returns or raises (the first failure in item order), so the caller may reuse the buffers
+    the calls wrote into."""
+    futs = [decode_pool().submit(fn, x) for x in items]
+    wait(futs)
+    return [f.result() for f in futs]
 
 
 def load_frames(files, indices=None, workers: int = 0, texture: bool = False):

@@ -195,8 +195,7 @@ def read_view_z(folder: str, files, need, pool: PinnedPool) -> HostView | None:
     def one(k):
         return L.slg_png_zstream(os.fsencode(files[need[k]]), ctypes.c_void_p(base + offs[k]), caps[k], infos[k])
     try:
-        with ThreadPoolExecutor(max_workers=min(FR.decode_threads(), len(need))) as ex:
-            rcs = list(ex.map(one, range(len(need))))
+        rcs = FR.decode_all(one, range(len(need)))
     except BaseException:
         pool.put(buf)                   # (a file vanished, an executor error): the buffer goes back
         raise
@@ -245,8 +244,11 @@ def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", 
             if a.shape != (H, W):
                 raise ValueError("all frames must have the same size")
             stack[i, :n_px].numpy()[:] = a.reshape(-1)
-        with ThreadPoolExecutor(max_workers=workers) as ex:
-            list(ex.map(one, need))
+        try:
+            FR.decode_all(one, need)
+        except BaseException:
+            pool.put(buf)                 # (every decode has stopped writing into it)
+            raise
         return HostView(folder, len(files), H, W, stride, "gray", stack, pinned=[buf])
     # colour (or non-PNG) captures: decoded RGB(A) frames, converted to gray on the device
     first = _decode_rgb(files[0])

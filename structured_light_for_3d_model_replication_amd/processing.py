@@ -357,10 +357,11 @@ class ProcessingLogic:
 
 def batch_views() -> int:
     """Views per batched launch in batch mode: ``SLG_BATCH_VIEWS`` (1..16), default 1.  The file
-    path is bound by host PNG decode and PLY formatting, not by the GPU (11 ms of 27 per C2
-    view): a group of 8 waits for 8 reads before its launch and measured 0.050 s/view against
-    0.0275 for 1 over 16 views (profiles/r2k/e2e_files.json); groups pay off for in-memory
-    sources (BatchReconstructor, bench.py)."""
+    path is bound by the host PNG decode (~70 C2 views/s on 16 CPUs), not by the GPU, and a
+    group waits for all its reads before its launch: over 36 C2 folders, groups of 1 / 4 / 8
+    measured 0.0135-0.0149 / 0.0138-0.0144 / 0.0143-0.0163 s/view with the device taking its
+    share of the PNGs, 0.0157 / 0.0161-0.0166 host-only (profiles/r5t/e2e.json).  Groups pay
+    off for in-memory sources (BatchReconstructor, bench.py)."""
     try:
         return max(1, min(16, int(os.environ.get("SLG_BATCH_VIEWS", "1"))))
     except ValueError:
