@@ -307,8 +307,12 @@ __device__ __attribute__((always_inline)) inline int64_t hist_at_least_wave(cons
 #define SLG_OTSU_MARK(k)                   // tools/otsu_probe.hip: a timestamp per part of otsu_wave
 #endif
 #ifndef SLG_OTSU_LDS
-#define SLG_OTSU_LDS 3                     // 3: broadcast LDS operands + v_cndmask capture (both chains);
-#endif                                     // 2: q1 by readlanes, mu1 from LDS; 1: both LDS-stored; 0: readlanes (round 4)
+#define SLG_OTSU_LDS 4                     // 4: as 3, one capture per 4 bins, the lanes redo their own bins;
+#endif                                     // 3: broadcast LDS operands + v_cndmask capture per bin (both chains);
+                                           // 2: q1 by readlanes, mu1 from LDS; 1: both LDS-stored; 0: readlanes (round 4)
+#ifndef SLG_OTSU_UNROLL
+#define SLG_OTSU_UNROLL 2                  // mode 4's chain loops: steps per loop body
+#endif
 constexpr int kOtsuLds = 7 * 256 + 128;   // 7 arrays of 256 bins + the chains' dump words
 constexpr int kOtsuChunk = 8;
 
@@ -402,7 +406,36 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
   SLG_OTSU_MARK(1);
   // 1. the q1 chain (OpenCV's order): LDS in, LDS out (wave-local: the wave's own LDS ops are
   // in order, the fence only keeps the compiler from moving them)
-#if SLG_OTSU_LDS == 3
+#if SLG_OTSU_LDS == 4
+  // as 3, but only the sum after each lane's 4 bins is captured (one 64-bit select per 4 adds);
+  // each lane then redoes its own 4 adds from its left neighbour's capture -- the same adds on
+  // the same values in the same order, so the same bits
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    double q1 = 0.0, qcap = 0.0;
+#pragma unroll SLG_OTSU_UNROLL
+    for (int l0 = 0; l0 < 64; l0 += 4) {
+      double pp[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) pp[k] = sp[4 * l0 + k];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q1 = q1 + pp[4 * t + j];
+        qcap = lane == l0 + t ? q1 : qcap;
+      }
+    }
+    double q = __shfl_up(qcap, 1);
+    if (lane == 0) q = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      q = q + pv[j];
+      q1r[j] = q;
+    }
+  }
+#elif SLG_OTSU_LDS == 3
   // operands as broadcast LDS reads, each bin's result captured into its owner lane's register
   // by v_cndmask: a dependent fp64 op costs ~5 clocks (tools/dp_latency_probe.hip), so a bin's
   // cost is its instruction count -- here one add and two selects
@@ -494,7 +527,76 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
   double mu1 = 0.0;
   SLG_OTSU_MARK(4);
   if (n_ok == hi - lo + 1 && n <= (int64_t(1) << 52)) {
-#if SLG_OTSU_LDS == 3
+#if SLG_OTSU_LDS == 4
+    {                                                // per bin {q1[i-1], ip, y, c}, 32 bytes
+      double* sops = lds + 256;
+      const double qprev0 = __shfl_up(q1r[3], 1);
+      double cr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double* o = sops + 4 * (4 * lane + j);
+        cr[j] = fma(-q1r[j], yr[j], 1.0) * yr[j];
+        o[0] = j == 0 ? qprev0 : q1r[j - 1];
+        o[1] = ip[j];
+        o[2] = yr[j];
+        o[3] = cr[j];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the chain over [lo, hi] (mu1 is 0 at lo, whatever q1[lo-1]), one capture per 4 bins:
+      // mcap of lane l = mu1 after bin min(4l + 3, hi)
+      double mu1c = 0.0, mcap = 0.0;
+      const int g_lo = lo >> 2, g_hi = hi >> 2;
+      // the edge groups (partial) apart, so the middle ones are one straight-line body the
+      // scheduler can unroll and issue the next group's LDS reads ahead in (an explicitly
+      // double-buffered form measured no faster: the buffers were shuffled through extra
+      // registers, profiles/r5x)
+      auto edge = [&](int l) {
+        double o[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) o[k] = sops[16 * l + k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * l + j;
+          if (i >= lo && i <= hi) {                  // (wave-uniform)
+            const double a = mu1c * o[4 * j] + o[4 * j + 1];
+            mu1c = fma(a, o[4 * j + 2], a * o[4 * j + 3]);
+          }
+        }
+        mcap = lane == l ? mu1c : mcap;
+      };
+      edge(g_lo);
+#pragma unroll SLG_OTSU_UNROLL
+      for (int l = g_lo + 1; l < g_hi; ++l) {
+        double o[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) o[k] = sops[16 * l + k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const double a = mu1c * o[4 * j] + o[4 * j + 1];
+          mu1c = fma(a, o[4 * j + 2], a * o[4 * j + 3]);
+        }
+        mcap = lane == l ? mu1c : mcap;
+      }
+      if (g_hi > g_lo) edge(g_hi);
+      // every lane redoes its own bins from its left neighbour's capture (0 before g_lo)
+      double m = __shfl_up(mcap, 1);
+      if (lane <= g_lo) m = 0.0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * lane + j;
+        const double qp = j == 0 ? qprev0 : q1r[j - 1];
+        const double a = m * qp + ip[j];
+        const double mj = fma(a, yr[j], a * cr[j]);
+        if (i >= lo && i <= hi) {
+          m = mj;
+          m1r[j] = mj;
+          ar[j] = a;
+        }
+      }
+    }
+#elif SLG_OTSU_LDS == 3
     {                                                // per bin {q1[i-1], ip, y, c}, 32 bytes
       double* sops = lds + 256;
       const double qprev0 = __shfl_up(q1r[3], 1);

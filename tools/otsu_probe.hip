@@ -9,6 +9,7 @@ __device__ unsigned long long g_otsu_marks[8];
 #define SLG_OTSU_MARK(k) (__builtin_amdgcn_s_waitcnt(0), g_otsu_marks[k] = __builtin_amdgcn_s_memtime())
 #include "../structured_light_for_3d_model_replication_amd/csrc/slgpu.hip"
 
+
 #include <float.h>
 #include <algorithm>
 #include <vector>
