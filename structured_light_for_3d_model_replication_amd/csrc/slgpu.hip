@@ -739,6 +739,9 @@ __device__ __attribute__((always_inline)) inline float percentile95_from_hist(co
 // (no carries between bytes: every byte stays in 1..16).  Lane maps checked by
 // tools/mfma_hist_probe.hip; C/D: col = lane & 15, row = 4 * (lane >> 4) + r.
 typedef int v4i32 __attribute__((ext_vector_type(4)));
+#ifndef SLG_HIST_UNROLL
+#define SLG_HIST_UNROLL 4
+#endif
 constexpr int kHistChunk = 1024;            // pixels per wave and MFMA chunk (16 per lane)
 constexpr int64_t kHistMaxChunks = 8000;    // per wave: 8000 * 1024 * 256 < 2^31 (i32 accumulators)
 
@@ -765,7 +768,8 @@ __device__ inline void mfma_hist_chunk(uint4* stage, const uint32_t (&w)[4], con
   stage[192 + lane] = make_uint4(d[0] & m4, d[1] & m4, d[2] & m4, d[3] & m4);
   // same-wave LDS accesses complete in order: no barrier between these writes and the reads
   const uint32_t repx = (uint32_t(lane & 15) * 0x01010101u) ^ m4;
-#pragma unroll
+  // (fully unrolled, the scheduler hoisted all 64 LDS reads: 307 VGPRs, one wave per SIMD)
+#pragma unroll SLG_HIST_UNROLL
   for (int i = 0; i < 16; ++i) {
     const int src = 4 * i + (lane >> 4);
     const uint4 hw = stage[src], lw = stage[64 + src], hd = stage[128 + src], ld = stage[192 + src];
@@ -800,7 +804,10 @@ __device__ inline void hist_load(const uint8_t* white, const uint8_t* black, int
   }
 }
 
-__global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
+#ifndef SLG_STATS_MINB
+#define SLG_STATS_MINB 1     // stats_kernel workgroups per CU its registers are budgeted for
+#endif
+__global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsParams p) {
   // 16 sub-histograms per kind (wave x lane&3), rows padded to 257 words so the copies of one
   // bin sit in different banks: a flat background costs at most 16-way same-address adds.
   constexpr int kRow = 257;
@@ -818,6 +825,21 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   uint32_t* hist_part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + kHistPartOff);
   uint64_t* states = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + states_off(p.n_px));
 
+#if SLG_SOLO_PROF
+  // (profiling builds: view 0's workgroups stamp [0] start, [1] counted, [2] atomics done,
+  // [3] ticket taken; the last arriver [4] sums read, [5] Otsu done, [6] end -- tools/solo_prof.py --stats)
+#define STATS_STAMP(k)                                                                                   \
+  do {                                                                                                   \
+    if (view == 0 && tid == 0 && blockIdx.x < 1024) g_solo_rec[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  if (view == 0 && tid == 0 && blockIdx.x < 1024)
+    for (int k = 4; k < 8; ++k) g_solo_rec[blockIdx.x * 8 + k] = 0;
+#else
+#define STATS_STAMP(k) \
+  do {             \
+  } while (0)
+#endif
+  STATS_STAMP(0);
   // Arm the compaction state of the following main launch (ordered by the kernel boundary).
   for (int64_t i = int64_t(blockIdx.x) * kBlock + tid; i < p.n_state_words; i += int64_t(gridDim.x) * kBlock)
     states[i] = 0;
@@ -894,6 +916,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   }
   if (!otsu) atomicMax(&s_maxd, local_max);
   __syncthreads();
+  STATS_STAMP(1);
   for (int i = tid; i < 2 * 256; i += kBlock) {
     const int kind = i >> 8, bin = i & 255;
     uint32_t v = 0;
@@ -914,6 +937,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   // (SLG_STATS_FENCE=1 restores the release / acquire fences).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  STATS_STAMP(2);
   if (tid == 0) {
     if (SLG_STATS_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -921,6 +945,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
     s_last = (t == gridDim.x - 1) ? 1u : 0u;
   }
   __syncthreads();
+  STATS_STAMP(3);
   if (!s_last) return;
 
   // Last arriver: read the global histograms, compute thresholds, reset for reuse.
@@ -941,6 +966,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
   }
   if (tid == 0) s_maxd = __hip_atomic_load(&ws->max_diff_enc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+  STATS_STAMP(4);
   if (otsu) {
     if (wave < 2) {                            // wave 0: white, wave 1: clip(w-b); concurrently
       const double thr = (p.dbg & 16) ? 100.0
@@ -965,8 +991,11 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(StatsParams p) {
     if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
     ws->above[tid] = p.n_px;                   // (the percentile histogram is black's: no bound)
   }
+  STATS_STAMP(5);
   for (int i = tid; i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
   if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
+  STATS_STAMP(6);
+#undef STATS_STAMP
 }
 
 // Otsu thresholds from the per-tile partial histograms a fused launch left in each view's

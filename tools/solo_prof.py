@@ -24,8 +24,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--xyz", default="f32")
+    ap.add_argument("--stats", action="store_true",
+                    help="time the one-view stats launch instead (stats_kernel's stamps: start, "
+                         "counted, atomics done, ticket; the last arriver's sums read, Otsu done, end)")
     args = ap.parse_args()
-    os.environ["SLG_SOLO"] = "1"                      # the one-view fused launch is opt-in
+    os.environ["SLG_SOLO"] = "0" if args.stats else "1"   # the one-view fused launch is opt-in
     import numpy as np
     import torch
     from structured_light_for_3d_model_replication_amd import _native as N, engine as E, synth
@@ -41,7 +44,7 @@ def main():
     lib = N.lib()
     rd = lib.slg_solo_prof_read
     rd.restype, rd.argtypes = ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int64]
-    n_wg = (H * W + 4095) // 4096
+    n_wg = (H * W + 4095) // 4096 if not args.stats else (H * W + 8191) // 8192   # stats: 8192 px per workgroup
     buf = np.zeros(1024 * 8, np.uint64)
     s = torch.cuda.current_stream()
     rows, kus = [], []
@@ -49,7 +52,10 @@ def main():
         buf[:] = 0
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(s)
-        eng.reconstruct(dfr[r % len(dfr)], cfg, dcal, 1, 2.0, out=out)
+        if args.stats:
+            eng.stats(dfr[r % len(dfr)], cfg)
+        else:
+            eng.reconstruct(dfr[r % len(dfr)], cfg, dcal, 1, 2.0, out=out)
         b.record(s)
         torch.cuda.synchronize()
         if rd(buf.ctypes.data, buf.size) != 0:
@@ -64,6 +70,18 @@ def main():
         rows.append((rel, fin))
     res = {"kernel_event_us_median": round(float(np.median(kus)), 2), "n_wg": n_wg, "error_flags": eng.error_flags()}
     allrel = np.concatenate([r for r, _ in rows])
+    if args.stats:
+        names = ["start", "counted", "atomics_done", "ticket"]
+        for i, nm in enumerate(names):
+            res[nm] = [round(float(np.percentile(allrel[:, i], q)), 2) for q in (0, 10, 50, 90, 100)]
+        last = []
+        for r, _ in rows:
+            k = int(np.argmax(r[:, 4]))                 # the last arriver (the only one with [4..6])
+            last.append([round(float(r[k, i]), 2) for i in range(7)])
+        res["last_arriver_stamps"] = last[:4]
+        res["last_arriver_what"] = "start, counted, atomics done, ticket, sums read, Otsu done, end (us)"
+        print(json.dumps(res), flush=True)
+        return
     for i, nm in enumerate(NAMES):
         res[nm] = [round(float(np.percentile(allrel[:, i], q)), 2) for q in (0, 10, 50, 90, 100)]
     for i, nm in enumerate(NAMES[1:], start=1):
