@@ -118,8 +118,8 @@ def device_png_enabled() -> bool:
 # a serial Huffman chain each; up to 768 streams in flight).  The device pays only when the host
 # has at least that long of its own work, ~26 views: the last n - 26 folders (at most 16) go to
 # ONE device launch started at the beginning, the host threads decode the rest meanwhile
-# (36 folders: 10 device views, 0.0156-0.0160 s/view against 0.0164-0.0166 host-only and
-# 0.0196-0.0234 with 16 device views, profiles/r5p).
+# (36 folders: 10 device views, 0.0135-0.0153 s/view against 0.0157-0.0160 host-only,
+# profiles/r5t, r6b; 16 device views were slower than host-only, profiles/r5p).
 HOST_AHEAD = 26
 DEVICE_MAX_VIEWS = 16
 
