@@ -165,3 +165,26 @@ def test_png_reserve_every_fits_the_device_group(monkeypatch):
     assert PL.png_reserve_every(800, 256) == 0
     monkeypatch.setenv("SLG_PNG_RESERVE_EVERY", "8")
     assert PL.png_reserve_every(44, 256) == 8
+
+
+def test_decode_all_waits_for_every_call_before_raising():
+    """frames.decode_all (the shared host decode pool): results in item order, and when a call
+    raises, every other call has finished before the exception reaches the caller -- the caller
+    then returns the pinned stack they wrote into to its pool (pipeline.read_view)."""
+    import threading
+    import time as _t
+    from structured_light_for_3d_model_replication_amd import frames as FR
+    assert FR.decode_all(lambda x: x * x, range(20)) == [x * x for x in range(20)]
+    done, lock = [], threading.Lock()
+
+    def work(i):
+        if i == 0:
+            raise ValueError("bad frame")
+        _t.sleep(0.05)
+        with lock:
+            done.append(i)
+        return i
+    with pytest.raises(ValueError, match="bad frame"):
+        FR.decode_all(work, range(8))
+    assert sorted(done) == list(range(1, 8))
+    assert FR.decode_pool() is FR.decode_pool()
