@@ -903,14 +903,17 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
         w[q] = *reinterpret_cast<const uint2*>(white + o);
         b[q] = *reinterpret_cast<const uint2*>(black + o);
       }
+      // (a guard, not a break: with the break the loop stayed rolled and w[] / b[] went to
+      // scratch, indexed at run time)
 #pragma unroll
       for (int k = 0; k < kStatsPx; ++k) {
-        if (px0 + k >= p.n_px) break;
-        const uint2 wq = w[k >> 3], bq = b[k >> 3];
-        const int wv = (((k & 7) < 4 ? wq.x : wq.y) >> (8 * (k & 3))) & 0xff;
-        const int bv = (((k & 7) < 4 ? bq.x : bq.y) >> (8 * (k & 3))) & 0xff;
-        atomicAdd(&h0[bv], 1u);
-        local_max = max(local_max, uint32_t(wv - bv + 256));
+        if (px0 + k < p.n_px) {
+          const uint2 wq = w[k >> 3], bq = b[k >> 3];
+          const int wv = (((k & 7) < 4 ? wq.x : wq.y) >> (8 * (k & 3))) & 0xff;
+          const int bv = (((k & 7) < 4 ? bq.x : bq.y) >> (8 * (k & 3))) & 0xff;
+          atomicAdd(&h0[bv], 1u);
+          local_max = max(local_max, uint32_t(wv - bv + 256));
+        }
       }
     }
   }
