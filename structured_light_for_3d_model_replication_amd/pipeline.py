@@ -128,18 +128,24 @@ _DECODE_STREAMS: dict = {}
 PNG_WAVES_PER_CU = 3        # png_inflate_kernel: one 64-lane wave per stream, ~50 KB of LDS each
 
 
+PNG_RESERVE_CHOICES = (3, 4, 8)   # CU-mask strides measured to keep the inflate at one launch latency
+
+
 def png_reserve_every(n_streams: int | None, n_cus: int) -> int:
-    """Every how-many-th CU the device PNG decode leaves to the other launches: the most CUs
-    (smallest k >= 2) whose complement still holds all ``n_streams`` inflate waves at once
-    (``PNG_WAVES_PER_CU`` each), so the fused launches of the host-decoded views beside it are not
-    squeezed onto a few CUs (16 free CUs made an 8-view group's kernels take ~100 ms instead of
-    ~8: profiles/r5p); 16 when the count is unknown.  SLG_PNG_RESERVE_EVERY overrides."""
+    """Every how-many-th CU the device PNG decode leaves to the other launches: the smallest
+    stride of ``PNG_RESERVE_CHOICES`` whose complement still holds all ``n_streams`` inflate waves
+    at once (``PNG_WAVES_PER_CU`` each), else 0 (a plain stream); 16 when the count is unknown.
+    The mask's CU numbering is the runtime's, not a plain CU index: strides 3, 4 and 8 kept a 10-
+    to 16-view launch at ~220 ms, while 6, 12 and 16 doubled it (370-390 ms) at counts that fit
+    on paper (tools/png_views_bench.py, profiles/r6e).  Leaving CUs out matters: with 16 free CUs
+    an 8-view group's fused launches took ~100 ms instead of ~8 (profiles/r5p).
+    SLG_PNG_RESERVE_EVERY overrides."""
     env = os.environ.get("SLG_PNG_RESERVE_EVERY")
     if env is not None:
         return int(env)
     if not n_streams:
         return 16
-    for k in range(2, 65):
+    for k in PNG_RESERVE_CHOICES:
         if (n_cus - n_cus // k) * PNG_WAVES_PER_CU >= n_streams:
             return k
     return 0                                         # more streams than fit: no CU left out

@@ -151,17 +151,18 @@ def test_resident_job_damage_reaches_every_overwritten_view():
 
 
 def test_png_reserve_every_fits_the_device_group(monkeypatch):
-    """The device PNG decode's CU mask leaves out as many CUs as it can while every inflate wave
-    of the group still fits (3 per CU): 10 C2 views (440 streams) leave every 3rd CU."""
+    """The device PNG decode's CU mask: the smallest measured-good stride (3, 4, 8) whose
+    complement holds every inflate wave of the group (3 per CU), else a plain stream."""
     from structured_light_for_3d_model_replication_amd import pipeline as PL
     monkeypatch.delenv("SLG_PNG_RESERVE_EVERY", raising=False)
     assert PL.png_reserve_every(None, 256) == 16
-    assert PL.png_reserve_every(440, 256) == 3
-    for n in (1, 44, 440, 528, 704, 720):
+    assert PL.png_reserve_every(440, 256) == 3       # 10 C2 views
+    assert PL.png_reserve_every(528, 256) == 4       # 12
+    assert PL.png_reserve_every(616, 256) == 8       # 14
+    assert PL.png_reserve_every(704, 256) == 0       # 16: a plain stream
+    for n in (1, 44, 440, 528, 616):
         k = PL.png_reserve_every(n, 256)
-        assert (256 - 256 // k) * PL.PNG_WAVES_PER_CU >= n
-        if k > 2:
-            assert (256 - 256 // (k - 1)) * PL.PNG_WAVES_PER_CU < n
+        assert k in PL.PNG_RESERVE_CHOICES and (256 - 256 // k) * PL.PNG_WAVES_PER_CU >= n
     assert PL.png_reserve_every(800, 256) == 0
     monkeypatch.setenv("SLG_PNG_RESERVE_EVERY", "8")
     assert PL.png_reserve_every(44, 256) == 8
