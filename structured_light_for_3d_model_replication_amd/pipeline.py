@@ -114,13 +114,13 @@ def device_png_enabled() -> bool:
 
 
 # Host PNG decode on the box's 16 CPUs: ~70 C2 views/s with two folders in flight (profiles/r5o,
-# 14 ms per view); one device inflate launch: ~230-400 ms whatever its size (one wave per stream,
-# a serial Huffman chain each; up to 768 streams in flight).  The device pays only when the host
-# has at least that long of its own work, ~26 views: the last n - 26 folders (at most 16) go to
-# ONE device launch started at the beginning, the host threads decode the rest meanwhile
-# (36 folders: 10 device views, 0.0135-0.0153 s/view against 0.0157-0.0160 host-only,
-# profiles/r5t, r6b; 16 device views were slower than host-only, profiles/r5p).
-HOST_AHEAD = 26
+# 14 ms per view); one device inflate launch: ~220 ms for up to 16 views on a CU mask from
+# png_reserve_every (one wave per stream, a serial Huffman chain each; the launch takes its
+# slowest stream's time).  The device pays only when the host has about that long of its own
+# work: the last n - 22 folders (at most 16) go to ONE device launch started at the beginning,
+# the host threads decode the rest meanwhile.  36 folders, 14 device views: 0.0133-0.0143 s/view,
+# against 0.0136-0.0174 with 10 and 0.0157-0.0177 host-only (profiles/r6g, r6h).
+HOST_AHEAD = 22
 DEVICE_MAX_VIEWS = 16
 
 
