@@ -632,8 +632,10 @@ class BatchPipeline:
         g.event.record(self.compute_stream)
         self.stats.span("launch", t, time.perf_counter(), f"{len(g.views)} views")
 
-    def _collect(self, g: _Group):
-        """Results of g's views as host (P float64 [N,3], C uint8 [N,3]) or exceptions."""
+    def _collect(self, g: _Group, ready=None):
+        """Results of g's views as host (P float64 [N,3], C uint8 [N,3]) or exceptions.
+        ``ready(k, result)``, when given, is called for each device-formatted view as soon as its
+        bytes are in host memory (its write can start while the group's later views copy)."""
         res = {}
         if not g.views:
             return res
@@ -682,6 +684,8 @@ class BatchPipeline:
                         host = self.pool.get((body.numel() + (16 << 20) - 1) // (16 << 20) * (16 << 20))
                         host[: body.numel()].copy_(body)
                         res[k] = FormattedCloud(n, host, body.numel(), self.pool)
+                        if ready is not None:
+                            ready(k, res[k])
         else:                                       # isolate the failing view(s)
             for k, hv, dev in g.views:
                 if k in redo:
@@ -793,6 +797,7 @@ class BatchPipeline:
             # ~10 ms per C2 view, profiles/r5n)
             writing: deque = deque()
             max_writing = max(3 * self.writers, 2 * self.group)
+            early_writes = os.environ.get("SLG_PIPE_EARLY_WRITES", "1") != "0"   # (A/B switch)
 
             def flush(block_until: int):
                 nonlocal success
@@ -812,19 +817,25 @@ class BatchPipeline:
                 if g is not None:
                     self._launch(g)
                 if prev is not None:
-                    res = self._collect(prev)
+                    early = {}                     # entry index -> its write, started early
+
+                    def ready(k, r, g=prev, early=early):
+                        early[k] = writer.submit(timed_write, g.entries[k][0], r)
+                    res = self._collect(prev, ready if early_writes else None)
                     done_imgs += sum(1 for _, fut in prev.entries if fut is not None)
                     prefetch(done_imgs + self.depth)
-                    writing.append((prev, self._submit_writes(prev, res, timed_write, writer)))
+                    writing.append((prev, self._submit_writes(prev, res, timed_write, writer, early)))
                     flush(max_writing)
                 prev = g
             flush(-1)
         return success
 
     @staticmethod
-    def _submit_writes(g: _Group, res, write, writer) -> dict:
-        """Start the group's PLY writes (writer threads): entry index -> (result, write future
-        or None, error)."""
+    def _submit_writes(g: _Group, res, write, writer, early=None) -> dict:
+        """Start the group's PLY writes (writer threads) not started yet (``early``: entry index
+        -> a write already started by :meth:`_collect`): entry index -> (result, write future or
+        None, error)."""
+        early = early or {}
         outcome = {}
         for k, (folder, fut) in enumerate(g.entries):
             if fut is None:
@@ -833,7 +844,11 @@ class BatchPipeline:
             r = res.get(k) if err is None else None
             if err is None and isinstance(r, Exception):
                 err = r
-            outcome[k] = (r, None if err is not None else writer.submit(write, folder, r), err)
+            if err is not None:
+                wf = None
+            else:
+                wf = early[k] if k in early else writer.submit(write, folder, r)
+            outcome[k] = (r, wf, err)
         return outcome
 
     def _log_group(self, g: _Group, outcome: dict) -> int:
