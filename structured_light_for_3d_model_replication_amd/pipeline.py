@@ -34,7 +34,7 @@ import os
 import threading
 import time
 from collections import deque
-from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import ThreadPoolExecutor, wait
 from dataclasses import dataclass, field
 
 
@@ -182,6 +182,19 @@ def device_share(n_folders: int, mode: str | None = None) -> int:
     return max(0, min(DEVICE_MAX_VIEWS, n_folders - ahead))
 
 
+_Z_POOL: list = []
+_Z_POOL_LOCK = threading.Lock()
+
+
+def _z_pool() -> ThreadPoolExecutor:
+    """The zlib-stream readers' pool (file read + chunk CRCs: light on CPU, kept off the decode
+    pool's queue)."""
+    with _Z_POOL_LOCK:
+        if not _Z_POOL:
+            _Z_POOL.append(ThreadPoolExecutor(max_workers=8, thread_name_prefix="slg-zread"))
+        return _Z_POOL[0]
+
+
 def read_view_z(folder: str, files, need, pool: PinnedPool) -> HostView | None:
     """Host half of the device PNG decode: the used frames' zlib streams (``slg_png_zstream``:
     file read + chunk CRCs, no inflate) packed into one pinned buffer, 256-byte aligned each.
@@ -201,7 +214,14 @@ def read_view_z(folder: str, files, need, pool: PinnedPool) -> HostView | None:
     def one(k):
         return L.slg_png_zstream(os.fsencode(files[need[k]]), ctypes.c_void_p(base + offs[k]), caps[k], infos[k])
     try:
-        rcs = FR.decode_all(one, range(len(need)))
+        # on a pool of their own by default: queued behind the host decoders' frames on the
+        # shared decode pool, the device group's streams (and so its launch) came later
+        if os.environ.get("SLG_Z_POOL", "own") == "shared":
+            rcs = FR.decode_all(one, range(len(need)))
+        else:
+            futs = [_z_pool().submit(one, k) for k in range(len(need))]
+            wait(futs)
+            rcs = [f.result() for f in futs]
     except BaseException:
         pool.put(buf)                   # (a file vanished, an executor error): the buffer goes back
         raise
