@@ -134,7 +134,7 @@ PNG_RESERVE_CHOICES = (3, 4, 8)   # CU-mask strides measured to keep the inflate
 def png_reserve_every(n_streams: int | None, n_cus: int) -> int:
     """Every how-many-th CU the device PNG decode leaves to the other launches: the smallest
     stride of ``PNG_RESERVE_CHOICES`` whose complement still holds all ``n_streams`` inflate waves
-    at once (``PNG_WAVES_PER_CU`` each), else 0 (a plain stream); 16 when the count is unknown.
+    at once (``PNG_WAVES_PER_CU`` each), else 0 (a plain stream); 8 when the count is unknown.
     The mask's CU numbering is the runtime's, not a plain CU index: strides 3, 4 and 8 kept a 10-
     to 16-view launch at ~220 ms, while 6, 12 and 16 doubled it (370-390 ms) at counts that fit
     on paper (tools/png_views_bench.py, profiles/r6e).  Leaving CUs out matters: with 16 free CUs
@@ -144,7 +144,7 @@ def png_reserve_every(n_streams: int | None, n_cus: int) -> int:
     if env is not None:
         return int(env)
     if not n_streams:
-        return 16
+        return 8
     for k in PNG_RESERVE_CHOICES:
         if (n_cus - n_cus // k) * PNG_WAVES_PER_CU >= n_streams:
             return k

@@ -155,7 +155,7 @@ def test_png_reserve_every_fits_the_device_group(monkeypatch):
     complement holds every inflate wave of the group (3 per CU), else a plain stream."""
     from structured_light_for_3d_model_replication_amd import pipeline as PL
     monkeypatch.delenv("SLG_PNG_RESERVE_EVERY", raising=False)
-    assert PL.png_reserve_every(None, 256) == 16
+    assert PL.png_reserve_every(None, 256) == 8
     assert PL.png_reserve_every(440, 256) == 3       # 10 C2 views
     assert PL.png_reserve_every(528, 256) == 4       # 12
     assert PL.png_reserve_every(616, 256) == 8       # 14
