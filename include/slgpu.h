@@ -146,6 +146,16 @@ typedef struct slg_cloud {
 
 int32_t slg_version(void);
 const char *slg_last_error(void);
+/* Digest of the sources and flags this library was built from (build.py: sha256 of every
+ * source, the header and the compile flags); _native.lib() refuses a library whose digest does
+ * not match the sources beside it. */
+const char *slg_build_id(void);
+/* The fused kernel's instance table, one line per instance ("<symbol>\t<0|1>\n", 1 = its device
+ * code is in the library's gfx950 code object) into buf (cap bytes, NUL-terminated; truncated
+ * lines are dropped).  Returns the number of instances missing, or -SLG_ERR_INVALID.  Launches
+ * of a missing instance return SLG_ERR_UNSUPPORTED instead of reaching the HIP runtime, which
+ * aborts on them.  Reads the library file only (no HIP call). */
+int32_t slg_kernel_table(char *buf, int64_t cap);
 
 /* Workspace size for images of n_pixels (covers every mode). */
 int64_t slg_workspace_bytes(int64_t n_pixels);

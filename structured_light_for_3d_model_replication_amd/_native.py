@@ -13,9 +13,18 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_NAME = "libslgpu.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-if os.environ.get("SLG_LIB"):            # A/B builds of the same ABI (tools/kbench.py); in-tree only
-    LIB_PATH = os.path.abspath(os.environ["SLG_LIB"])
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+# A/B builds of the same ABI (tools/build_ab.sh -> ab_libs/, build_ab/; tools/kbench.py, ab.py):
+# only libraries inside those in-tree build directories may replace the product library
+AB_DIRS = (os.path.join(REPO_DIR, "ab_libs"), os.path.join(REPO_DIR, "build_ab"))
+AB_LIB = None
+if os.environ.get("SLG_LIB"):
+    _p = os.path.realpath(os.environ["SLG_LIB"])
+    if not any(os.path.commonpath([_p, os.path.realpath(d)]) == os.path.realpath(d) for d in AB_DIRS):
+        raise ImportError(f"SLG_LIB={_p}: A/B libraries must live in {' or '.join(AB_DIRS)}")
+    LIB_PATH = AB_LIB = _p
 
 ABI_VERSION = 2          # SLG_ABI_VERSION in include/slgpu.h
 SLG_OK = 0
@@ -75,6 +84,8 @@ PNG_E_STREAM, PNG_E_SIZE, PNG_E_ADLER, PNG_E_FILTER, PNG_E_UNSUPPORTED = 1, 2, 3
 
 EXPORTS = {
     "slg_version": (c_i32, []),
+    "slg_build_id": (ctypes.c_char_p, []),
+    "slg_kernel_table": (c_i32, [ctypes.c_char_p, c_i64]),
     "slg_last_error": (ctypes.c_char_p, []),
     "slg_workspace_bytes": (c_i64, [c_i64]),
     "slg_workspace_init": (c_i32, [c_vp, c_i64, c_vp]),
@@ -151,13 +162,33 @@ def lib():
                               f"g.build()'` (hipcc --offload-arch=gfx950) first")
         h = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in EXPORTS.items():
+            if AB_LIB is not None and not hasattr(h, name):
+                continue                     # an A/B build from an older tree (tools/ab.py)
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
         if h.slg_version() != ABI_VERSION:
             raise ImportError("libslgpu ABI version mismatch")
+        if AB_LIB is None:
+            # provenance: the product library must be the build of the sources beside it
+            from . import build as B
+            built, want = h.slg_build_id().decode(), B.BUILD_ID_PREFIX.decode() + B.source_digest()
+            if built != want:
+                raise ImportError(f"{LIB_PATH} was built from other sources ({built}, sources {want}): "
+                                  "rebuild it (__graft_entry__.build())")
         _lib = h
     return _lib
+
+
+def kernel_table() -> dict:
+    """``{symbol: present}`` of the fused kernel's instance table (``slg_kernel_table``)."""
+    buf = ctypes.create_string_buffer(1 << 16)
+    lib().slg_kernel_table(buf, len(buf))
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, flag = line.split("\t")
+        out[name] = flag == "1"
+    return out
 
 
 def check(rc: int):

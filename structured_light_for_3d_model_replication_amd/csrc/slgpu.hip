@@ -40,6 +40,9 @@
 #include <unistd.h>
 #include <thread>
 #include <vector>
+#include <algorithm>
+#include <mutex>
+#include <dlfcn.h>
 
 #include "../../include/slgpu.h"
 
@@ -57,10 +60,6 @@ constexpr int kTileBlock = SLG_TILE_BLOCK;  // main3 workgroup: 512 lanes, 322.6
 constexpr int kTilePx = kTileBlock * kPx;   // 4096 pixels per main3 tile (one look-back entry)
 constexpr int kMapsPx = kBlock * kPx;       // 2048 pixels per decode_maps workgroup
 constexpr int kMaxBits = 15;                // packed 16-bit code lanes
-#ifndef SLG_LOOK_K
-#define SLG_LOOK_K 2
-#endif
-constexpr int kLookK = SLG_LOOK_K;         // look-back window = kLookK x 64 predecessor tiles per poll
 constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagInc = 2ull << 62;
 constexpr uint64_t kValMask = (1ull << 62) - 1;
@@ -71,7 +70,7 @@ struct WsHeader {
   uint32_t max_diff_enc;   // max(white-black) + 256 (0 = none yet)
   uint32_t ticket;         // stats_kernel arrival counter
   uint32_t tile_counter;   // next (view, tile) id of a main3 launch (this slice = its view 0)
-  uint32_t error;          // bit 0: look-back spin timeout; 1: a look-back helper ran; 2: SOLO threshold wait gave up
+  uint32_t error;          // bit 0: look-back spin timeout; 1: a look-back helper ran
   int32_t smin;            // mask: white >= smin
   int32_t cmin;            //       (white - black) >= cmin
   int32_t pad0[2];
@@ -82,9 +81,7 @@ struct WsHeader {
   // which the clipped histogram cannot count); their minimum bounds the valid pixels, so the
   // point count of row_mode 0/1 (resident jobs size their clouds with it).  n_px otherwise.
   int64_t above[2];
-  // one-view fused launches (main3 SOLO): [0] chunk claims, [1] chunks counted, [2] workgroups
-  // exited, [3] thresholds ready; the launch's last workgroup to exit zeroes them again
-  uint32_t solo[4];
+  uint32_t reserved[4];
   uint64_t pad3[4];
 };
 constexpr int kHistCopies = 16;            // partial histograms: blocks spread their atomics
@@ -170,37 +167,14 @@ constexpr int kStatsBlocks = 64;            // stats workgroups per view (at mos
 #define SLG_STATS_OTSU_BLOCKS 64                 // 128: 2.6% and 256: 10% slower bench (slot contention)
 #endif
 constexpr int kStatsBlocksOtsu = SLG_STATS_OTSU_BLOCKS;   // matrix-core Otsu path
-#ifndef SLG_STATS_ABL
-#define SLG_STATS_ABL 0   // profiling ablations (tools/gpu_r3aq.sh): 1 no MFMA, 2 no merge
+#ifndef SLG_STATS_BLOCKS_ONE
+#define SLG_STATS_BLOCKS_ONE 256   // r3ao: 64 -> 51.7, 128 -> 42.2, 256 -> 40.0, 512 -> 39.9 us (1080p, Otsu)
 #endif
-#ifndef SLG_STATS_BLOCKS_SOLO
-#define SLG_STATS_BLOCKS_SOLO 256   // r3ao: 64 -> 51.7, 128 -> 42.2, 256 -> 40.0, 512 -> 39.9 us (1080p, Otsu)
+constexpr int kStatsBlocksOne = SLG_STATS_BLOCKS_ONE;   // one-view launches (nothing runs beside them)
+#ifndef SLG_OTSU_ONE_CHUNKS
+#define SLG_OTSU_ONE_CHUNKS 2
 #endif
-constexpr int kStatsBlocksSolo = SLG_STATS_BLOCKS_SOLO;   // one-view launches (nothing runs beside them)
-#ifndef SLG_OTSU_SOLO_CHUNKS
-#define SLG_OTSU_SOLO_CHUNKS 2
-#endif
-constexpr int kOtsuSoloChunks = SLG_OTSU_SOLO_CHUNKS;
-// SLG_SOLO_PROF=1 (A/B builds only, tools/solo_prof.py): per-workgroup s_memrealtime stamps of a
-// one-view fused launch -- [0] start, [1] stats done, [2] frame loads issued, [3] thresholds
-// seen, [4] phase A done, [5] exit; the finisher adds [6] Otsu start, [7] flag raised.
-#ifndef SLG_STATS_FENCE
-#define SLG_STATS_FENCE 0   // release / acquire fences around the stats tickets (atomics only: unneeded)
-#endif
-#ifndef SLG_SOLO_PROF
-#define SLG_SOLO_PROF 0
-#endif
-#if SLG_SOLO_PROF
-__device__ uint64_t g_solo_rec[1024 * 8];
-#define SOLO_STAMP(k)                                                                  \
-  do {                                                                                 \
-    if (threadIdx.x == 0 && blockIdx.x < 1024) g_solo_rec[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define SOLO_STAMP(k) \
-  do {            \
-  } while (0)
-#endif
+constexpr int kOtsuOneChunks = SLG_OTSU_ONE_CHUNKS;
 
 struct StatsParams {
   const uint8_t* white[kMaxBatch];
@@ -212,8 +186,7 @@ struct StatsParams {
   int32_t pad;
   double shadow_val;
   double contrast_val;
-  int32_t dbg;             // profiling ablation (SLG_DBG bit 4: skip the Otsu tail)
-  int32_t pad2;
+  int32_t pad2[2];
   const uint32_t* parts[kMaxBatch];   // parts_kernel: per-tile partial histograms of each view
   int64_t n_parts;                    // tiles per view
   int64_t pad_zero;                   // zero pixels counted past n_px (removed from bin 0)
@@ -252,15 +225,10 @@ __device__ inline double readlane_f64(double v, int l) {
   return __longlong_as_double((long long)((uint64_t(hi) << 32) | lo));
 }
 
-// otsu_wave's mu1 run over bins [lo, hi].  SPEC: each quotient as fma(a, y, a * y_lo), where
-// y + y_lo = 1/q1 to ~2^-105 (1 - q1 y is exact; y_lo off the chain): 2 dependent ops instead
-// of div_rn's 5.  The result is faithful, and
-// RN(a / q1) unless a / q1 sits within ~2^-105 of a rounding boundary, so the caller checks every
-// bin afterwards (Markstein: RN(m + (a - q1 m) y) = RN(a / q1) for faithful m) and reruns
-// without SPEC on a miss.  ar keeps each bin's numerator for that check.
-template <bool SPEC>
-__device__ inline void mu1_run(int lo, int hi, const double (&ip)[4], const double (&q1r)[4], const double (&yr)[4],
-                               double (&m1r)[4], double (&ar)[4]) {
+// otsu_wave's exact mu1 run over bins [lo, hi] (the rerun when the speculative chain misses):
+// each quotient as the Markstein pair div_rn(a, q1, y).
+__device__ inline void mu1_run_exact(int lo, int hi, const double (&ip)[4], const double (&q1r)[4],
+                                     const double (&yr)[4], double (&m1r)[4]) {
   const int lane = threadIdx.x & 63;
   double mu1 = 0.0, q_prev = 0.0;                    // bin i's previous q1 is bin i-1's q1 (mu1 = 0 at lo)
   for (int l = lo >> 2; l <= (hi >> 2); ++l) {
@@ -270,15 +238,8 @@ __device__ inline void mu1_run(int lo, int hi, const double (&ip)[4], const doub
       if (i < lo || i > hi) continue;                // scalar: first and last lane only
       const double a = mu1 * q_prev + readlane_f64(ip[j], l);
       q_prev = readlane_f64(q1r[j], l);
-      const double y = readlane_f64(yr[j], l);
-      if (SPEC)
-        mu1 = fma(a, y, a * (fma(-q_prev, y, 1.0) * y));
-      else
-        mu1 = div_rn(a, q_prev, y);
-      if (lane == l) {
-        m1r[j] = mu1;
-        if (SPEC) ar[j] = a;
-      }
+      mu1 = div_rn(a, q_prev, readlane_f64(yr[j], l));
+      if (lane == l) m1r[j] = mu1;
     }
   }
 }
@@ -298,97 +259,27 @@ __device__ __attribute__((always_inline)) inline int64_t hist_at_least_wave(cons
   return int64_t(wave_sum(a));
 }
 
-// The two serial chains of otsu_wave run on wave-uniform registers fed from LDS: every lane
-// computes the same chain, its per-bin operands read as broadcast LDS words a chunk ahead, and
-// lane 0 stores the per-bin results back.  A step is then the chain's own fp64 ops and nothing
-// else (the readlane variant paid two v_readlane, their SGPR hazard and two v_cndmask per bin).
-// lds: kOtsuLds doubles of this wave's own.
+// The two serial chains of otsu_wave (q1, then mu1) run on wave-uniform registers fed from LDS:
+// every lane computes the same chain, its per-bin operands read as broadcast LDS words, and only
+// the value after each lane's four bins is captured (one 64-bit select per four steps); each
+// lane then redoes its own four steps from its left neighbour's capture -- the same operations on
+// the same values in the same order, so the same bits.  A dependent fp64 op costs ~5 clocks
+// (tools/dp_latency_probe.hip), so a step costs its instruction count (profiles/r5y: 7.8 us for
+// one 1080p histogram).  lds: kOtsuLds doubles of this wave's own.
 #ifndef SLG_OTSU_MARK
 #define SLG_OTSU_MARK(k)                   // tools/otsu_probe.hip: a timestamp per part of otsu_wave
 #endif
-#ifndef SLG_OTSU_LDS
-#define SLG_OTSU_LDS 4                     // 4: as 3, one capture per 4 bins, the lanes redo their own bins;
-#endif                                     // 3: broadcast LDS operands + v_cndmask capture per bin (both chains);
-                                           // 2: q1 by readlanes, mu1 from LDS; 1: both LDS-stored; 0: readlanes (round 4)
 #ifndef SLG_OTSU_UNROLL
-#define SLG_OTSU_UNROLL 2                  // mode 4's chain loops: steps per loop body
+#define SLG_OTSU_UNROLL 2                  // the chain loops: steps per loop body
 #endif
-constexpr int kOtsuLds = 7 * 256 + 128;   // 7 arrays of 256 bins + the chains' dump words
-constexpr int kOtsuChunk = 8;
+constexpr int kOtsuLds = 5 * 256;          // p_i [256] + the mu1 chain's {q1[i-1], ip, y, c} [256][4]
 
-// q1[i] = q1[i-1] + p[i] in bin order (OpenCV's sequential sum), p and q1 in LDS.  Every lane
-// stores every step -- lane 0 to sq[i], the others to a dump word of their own -- so the loop
-// has no per-bin branch (an `if (lane == 0)` store cost two taken branches per bin).
-__device__ __attribute__((always_inline)) inline void q1_chain_lds(const double* sp, double* sq, double* dump) {
-  const int lane = threadIdx.x & 63;
-  double q1 = 0.0;
-#pragma unroll 1
-  for (int i0 = 0; i0 < 256; i0 += kOtsuChunk) {
-    double pp[kOtsuChunk];
-#pragma unroll
-    for (int k = 0; k < kOtsuChunk; ++k) pp[k] = sp[i0 + k];
-#pragma unroll
-    for (int k = 0; k < kOtsuChunk; ++k) {
-      q1 = q1 + pp[k];
-      *(lane == 0 ? sq + i0 + k : dump + lane) = q1;
-    }
-  }
-}
-
-// mu1_run<true> on LDS operands, over bins [lo, hi]: a = mu1 * q1[i-1] + ip[i] (mu1 = 0 at lo,
-// where q1[lo-1] is taken as 0 as mu1_run does) as the reference rounds it, then
-// mu1 = fma(a, y[i], e) with e = fma(mu1, qc[i], ipc[i]) ~ a * c[i] (qc = q1[i-1] c, ipc = ip c,
-// c = fma(-q1, y, 1) y, all precomputed): e is only the ~2^-53-relative correction of a y, so
-// computing it from mu1 instead of from the rounded a changes the result only where a / q1 lies
-// within ~2^-104 of a rounding boundary, which the caller's check catches.  Three dependent fp64
-// ops per bin (mul, add, fma) instead of four.  Every bin's a and mu1 stored for the check
-// (branch-free, as q1_chain_lds).
-__device__ __attribute__((always_inline)) inline void mu1_chain_lds(int lo, int hi, const double* sq, const double* sip,
-                                                                    const double* sy, const double* sqc,
-                                                                    const double* sipc, double* sa, double* sm,
-                                                                    double* dump) {
-  const int lane = threadIdx.x & 63;
-  constexpr int C = 4;
-  double mu1 = 0.0;
-#pragma unroll 1
-  for (int i0 = lo; i0 <= hi; i0 += C) {
-    double qp[C], ipk[C], yk[C], qck[C], ipck[C];
-#pragma unroll
-    for (int k = 0; k < C; ++k) {
-      const int i = i0 + k <= hi ? i0 + k : hi;        // (past hi: computed, never stored)
-      qp[k] = i > lo ? sq[i - 1] : 0.0;
-      ipk[k] = sip[i]; yk[k] = sy[i]; qck[k] = i > lo ? sqc[i] : 0.0; ipck[k] = sipc[i];
-    }
-#pragma unroll
-    for (int k = 0; k < C; ++k) {
-      const double m = mu1 * qp[k];
-      const double e = fma(mu1, qck[k], ipck[k]);
-      const double a = m + ipk[k];
-      mu1 = fma(a, yk[k], e);
-      const bool mine = lane == 0 && i0 + k <= hi;
-      *(mine ? sa + i0 + k : dump + lane) = a;
-      *(mine ? sm + i0 + k : dump + 64 + lane) = mu1;
-    }
-  }
-}
-
-#ifndef SLG_OTSU_PRIO
-#define SLG_OTSU_PRIO 0     // s_setprio of the Otsu waves (the chains are issue-bound), 0: none
-#endif
 __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t* h, int64_t n, double* lds) {
-  if (SLG_OTSU_PRIO) __builtin_amdgcn_s_setprio(SLG_OTSU_PRIO);
   SLG_OTSU_MARK(0);
   const int lane = threadIdx.x & 63;
   const double scale = 1.0 / double(n);
   const double eps = double(__FLT_EPSILON__);
   double* sp = lds;                 // p_i
-  double* sq = lds + 256;           // q1_i
-  double* sip = lds + 512;          // i * p_i
-  double* sy = lds + 768;           // RN(1 / q1_i) of unskipped bins
-  double* sqc = lds + 1024;         // q1_{i-1} * c_i, c_i = fma(-q1_i, y_i, 1) * y_i
-  double* sa = lds + 1280;          // the mu1 chain's numerators
-  double* sm = lds + 1536;          // and its mu1 values
-  double* sipc = lds;               // ip_i * c_i (over p_i, which only the q1 chain reads)
   double pv[4], ip[4], q1r[4], yr[4], m1r[4], ar[4];
   uint64_t isum = 0;
 #pragma unroll
@@ -399,17 +290,12 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
     isum += uint64_t(i) * h[i];
     q1r[j] = yr[j] = m1r[j] = ar[j] = 0.0;
     sp[i] = pv[j];
-    sip[i] = ip[j];
   }
   isum = wave_sum(isum);
   const double mu = double(isum) * scale;
   SLG_OTSU_MARK(1);
-  // 1. the q1 chain (OpenCV's order): LDS in, LDS out (wave-local: the wave's own LDS ops are
-  // in order, the fence only keeps the compiler from moving them)
-#if SLG_OTSU_LDS == 4
-  // as 3, but only the sum after each lane's 4 bins is captured (one 64-bit select per 4 adds);
-  // each lane then redoes its own 4 adds from its left neighbour's capture -- the same adds on
-  // the same values in the same order, so the same bits
+  // 1. the q1 chain (OpenCV's order) from broadcast LDS reads (wave-local: the wave's own LDS ops
+  // are in order, the fence only keeps the compiler from moving them)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -435,55 +321,6 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
       q1r[j] = q;
     }
   }
-#elif SLG_OTSU_LDS == 3
-  // operands as broadcast LDS reads, each bin's result captured into its owner lane's register
-  // by v_cndmask: a dependent fp64 op costs ~5 clocks (tools/dp_latency_probe.hip), so a bin's
-  // cost is its instruction count -- here one add and two selects
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  {
-    double q1 = 0.0;
-#pragma unroll 1
-    for (int l0 = 0; l0 < 64; l0 += 4) {
-      double pp[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) pp[k] = sp[4 * l0 + k];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bool mine = lane == l0 + t;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          q1 = q1 + pp[4 * t + j];
-          q1r[j] = mine ? q1 : q1r[j];
-        }
-      }
-    }
-  }
-#elif SLG_OTSU_LDS == 1
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  q1_chain_lds(sp, sq, lds + 7 * 256);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-  for (int j = 0; j < 4; ++j) q1r[j] = sq[4 * lane + j];
-#else
-  // the readlane chain: 36 clocks per bin against 51 for q1_chain_lds (tools/otsu_probe.hip,
-  // profiles/r5g) -- its operand and result moves are independent of the chain
-  double q1 = 0.0;
-  for (int l = 0; l < 64; ++l) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const double nq = q1 + readlane_f64(pv[j], l);
-      if (lane == l) q1r[j] = nq;
-      q1 = nq;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) sq[4 * lane + j] = q1r[j];
-#endif
   SLG_OTSU_MARK(2);
   uint32_t okr = 0;                                  // 2. bit j: bin 4*lane+j not skipped
 #pragma unroll
@@ -494,26 +331,16 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
       yr[j] = 1.0 / q1r[j];
     }
   }
-#if SLG_OTSU_LDS == 1 || SLG_OTSU_LDS == 2
-  {                                                  // the mu1 chain's precomputed operands
-    const double q_last_prev = __shfl_up(q1r[3], 1); // q1 of bin 4 lane - 1 (lane 0: unused)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const double c = fma(-q1r[j], yr[j], 1.0) * yr[j];
-      const double qprev = j == 0 ? q_last_prev : q1r[j - 1];
-      sy[4 * lane + j] = yr[j];
-      sqc[4 * lane + j] = qprev * c;
-      sipc[4 * lane + j] = ip[j] * c;
-    }
-  }
-#endif
   // 3. the mu1 chain.  The unskipped bins form one run [lo, hi]: q1 never decreases and
   // q2 = RN(1 - q1) never increases, so each skip test holds on a prefix plus a suffix of the
-  // bins, and mu1 is still 0 at lo.  Over the run every bin is the same 4 dependent ops
-  // (mu1_run<true>, checked afterwards; 7 in mu1_run<false>) with no per-bin test when every
-  // numerator suits div_rn: a is 0, or at least ~1/n (an empty bin's mu1 *= q1 then / q1 moves
-  // a by ulps), so n <= 2^52 keeps a far inside its range.  Anything else (never seen) takes the
-  // general loop: per-bin skip flags, IEEE division when refused.
+  // bins, and mu1 is still 0 at lo.  Over the run every bin is the same few dependent ops,
+  // each quotient taken speculatively as fma(a, y, a * c) with c = fma(-q1, y, 1) * y (y + c
+  // is 1/q1 to ~2^-105): faithful, and RN(a / q1) unless a / q1 sits within ~2^-105 of a
+  // rounding boundary -- so every bin is checked afterwards (Markstein: RN(m + (a - q1 m) y)
+  // = RN(a / q1) for faithful m) and the run is redone exactly on a miss.  That needs every
+  // numerator to suit div_rn: a is 0, or at least ~1/n (an empty bin's mu1 *= q1 then / q1
+  // moves a by ulps), so n <= 2^52 keeps a far inside its range.  Anything else (never seen)
+  // takes the general loop: per-bin skip flags, IEEE division when refused.
   SLG_OTSU_MARK(3);
   const uint64_t lanes_ok = __ballot(okr != 0);
   int lo = 256, hi = -1, n_ok = 0;
@@ -527,7 +354,6 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
   double mu1 = 0.0;
   SLG_OTSU_MARK(4);
   if (n_ok == hi - lo + 1 && n <= (int64_t(1) << 52)) {
-#if SLG_OTSU_LDS == 4
     {                                                // per bin {q1[i-1], ip, y, c}, 32 bytes
       double* sops = lds + 256;
       const double qprev0 = __shfl_up(q1r[3], 1);
@@ -596,56 +422,6 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
         }
       }
     }
-#elif SLG_OTSU_LDS == 3
-    {                                                // per bin {q1[i-1], ip, y, c}, 32 bytes
-      double* sops = lds + 256;
-      const double qprev0 = __shfl_up(q1r[3], 1);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        double* o = sops + 4 * (4 * lane + j);
-        o[0] = j == 0 ? qprev0 : q1r[j - 1];
-        o[1] = ip[j];
-        o[2] = yr[j];
-        o[3] = fma(-q1r[j], yr[j], 1.0) * yr[j];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      double mu1c = 0.0;                             // = mu1_run<true>: 0 at lo, whatever q1[lo-1]
-#pragma unroll 1
-      for (int l = lo >> 2; l <= (hi >> 2); ++l) {
-        double o[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) o[k] = sops[16 * l + k];
-        const bool mine = lane == l;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int i = 4 * l + j;
-          const bool act = i >= lo && i <= hi;       // wave-uniform
-          const double a = mu1c * o[4 * j] + o[4 * j + 1];
-          const double m = fma(a, o[4 * j + 2], a * o[4 * j + 3]);
-          mu1c = act ? m : mu1c;
-          m1r[j] = (mine && act) ? m : m1r[j];
-          ar[j] = (mine && act) ? a : ar[j];
-        }
-      }
-    }
-#elif SLG_OTSU_LDS
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // (1, 2: the mu1 chain from LDS)
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    mu1_chain_lds(lo, hi, sq, sip, sy, sqc, sipc, sa, sm, lds + 7 * 256);   // ~ mu1_run<true>(lo, hi, ...)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = 4 * lane + j;
-      if (i >= lo && i <= hi) { m1r[j] = sm[i]; ar[j] = sa[i]; }
-    }
-#else
-    mu1_run<true>(lo, hi, ip, q1r, yr, m1r, ar);
-#endif
     SLG_OTSU_MARK(5);
     uint32_t miss = 0;
 #pragma unroll
@@ -653,7 +429,7 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
       const double r = fma(-q1r[j], m1r[j], ar[j]);   // exact remainder
       if ((okr >> j) & 1u) miss |= uint32_t(fma(r, yr[j], m1r[j]) != m1r[j]);
     }
-    if (__ballot(miss != 0)) mu1_run<false>(lo, hi, ip, q1r, yr, m1r, ar);
+    if (__ballot(miss != 0)) mu1_run_exact(lo, hi, ip, q1r, yr, m1r);
   } else {
     const int l_end = 64 - __builtin_clzll(lanes_ok | 1ull);   // lanes with work: [0, l_end)
     double q_prev = 0.0;
@@ -690,7 +466,6 @@ __device__ __attribute__((always_inline)) inline double otsu_wave(const uint32_t
     if (ob > best || (ob == best && oi < best_i)) { best = ob; best_i = oi; }
   }
   SLG_OTSU_MARK(7);
-  if (SLG_OTSU_PRIO) __builtin_amdgcn_s_setprio(0);
   return best_i == INT_MAX ? 0.0 : double(best_i);
 }
 
@@ -825,21 +600,6 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
   uint32_t* hist_part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + kHistPartOff);
   uint64_t* states = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + states_off(p.n_px));
 
-#if SLG_SOLO_PROF
-  // (profiling builds: view 0's workgroups stamp [0] start, [1] counted, [2] atomics done,
-  // [3] ticket taken; the last arriver [4] sums read, [5] Otsu done, [6] end -- tools/solo_prof.py --stats)
-#define STATS_STAMP(k)                                                                                   \
-  do {                                                                                                   \
-    if (view == 0 && tid == 0 && blockIdx.x < 1024) g_solo_rec[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-  if (view == 0 && tid == 0 && blockIdx.x < 1024)
-    for (int k = 4; k < 8; ++k) g_solo_rec[blockIdx.x * 8 + k] = 0;
-#else
-#define STATS_STAMP(k) \
-  do {             \
-  } while (0)
-#endif
-  STATS_STAMP(0);
   // Arm the compaction state of the following main launch (ordered by the kernel boundary).
   for (int64_t i = int64_t(blockIdx.x) * kBlock + tid; i < p.n_state_words; i += int64_t(gridDim.x) * kBlock)
     states[i] = 0;
@@ -872,11 +632,7 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
       uint32_t wn[4], dn[4];
       const bool more = c + step < p.n_px;
       if (more) hist_load(white, black, c + step, p.n_px, wn, dn);
-#if SLG_STATS_ABL & 1
-      acc_w[0] += int(w[0] ^ d[1]);
-#else
       mfma_hist_chunk(s_stage + wave * 256, w, d, acc_w, acc_d);
-#endif
       if (more) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) { w[q] = wn[q]; d[q] = dn[q]; }
@@ -919,44 +675,34 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
   }
   if (!otsu) atomicMax(&s_maxd, local_max);
   __syncthreads();
-  STATS_STAMP(1);
   for (int i = tid; i < 2 * 256; i += kBlock) {
     const int kind = i >> 8, bin = i & 255;
     uint32_t v = 0;
 #pragma unroll
     for (int c = 0; c < 16; ++c) v += sh[(2 * c + kind) * kRow + bin];
-#if SLG_STATS_ABL & 2
-    if (v == 0xffffffffu)
-#else
-    if (v)
-#endif
-      atomicAdd(hist_part + (blockIdx.x % kHistCopies) * 512 + i, v);
+    if (v) atomicAdd(hist_part + (blockIdx.x % kHistCopies) * 512 + i, v);
   }
   if (!otsu && tid == 0 && s_maxd) atomicMax(&ws->max_diff_enc, s_maxd);
 
-  // Publish (every wave drains its atomics, barrier) then take a ticket.  What the last arriver
-  // reads -- the histogram copies, max_diff_enc -- is written and read by agent-scope atomics
-  // only, performed at the point of coherence once vmcnt says so: no L2 write-back / invalidate
-  // (SLG_STATS_FENCE=1 restores the release / acquire fences).
+  // Publish (every wave drains its atomics, barrier) then take a ticket.  Hardware assumption
+  // (no release / acquire fences): what the last arriver reads -- the histogram copies,
+  // max_diff_enc -- is written and read by agent-scope atomics only, which gfx950 performs at
+  // the L2 that owns the address (the device's point of coherence for agent scope, whichever
+  // XCD issues them); a returned vmcnt means the add has been performed there, so a ticket
+  // taken after vmcnt(0) orders every earlier add before the last arriver's atomic loads.  No
+  // L2 write-back or invalidate is needed (an agent-scope fence is one of each, per workgroup).
+  // tests/test_gpu_configs.py::test_concurrent_stats_thresholds checks the thresholds of many
+  // concurrent multi-view launches against the oracle.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  STATS_STAMP(2);
   if (tid == 0) {
-    if (SLG_STATS_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t t = __hip_atomic_fetch_add(&ws->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (t == gridDim.x - 1) ? 1u : 0u;
   }
   __syncthreads();
-  STATS_STAMP(3);
   if (!s_last) return;
 
   // Last arriver: read the global histograms, compute thresholds, reset for reuse.
-  if (SLG_STATS_FENCE && tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
   uint32_t* hg = sh;                           // reuse the sub-histograms for the global ones
   for (int i = tid; i < 2 * 256; i += kBlock)
   {
@@ -969,11 +715,9 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
   }
   if (tid == 0) s_maxd = __hip_atomic_load(&ws->max_diff_enc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  STATS_STAMP(4);
   if (otsu) {
     if (wave < 2) {                            // wave 0: white, wave 1: clip(w-b); concurrently
-      const double thr = (p.dbg & 16) ? 100.0
-                         : otsu_wave(hg + 256 * wave, p.n_px, reinterpret_cast<double*>(sh + 512) + wave * kOtsuLds);
+      const double thr = otsu_wave(hg + 256 * wave, p.n_px, reinterpret_cast<double*>(sh + 512) + wave * kOtsuLds);
       const int m = int_threshold(thr, wave == 0 ? 0 : -255);
       const int64_t above = hist_at_least_wave(hg + 256 * wave, m, p.n_px);
       if ((tid & 63) == 0) {
@@ -994,11 +738,8 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
     if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
     ws->above[tid] = p.n_px;                   // (the percentile histogram is black's: no bound)
   }
-  STATS_STAMP(5);
   for (int i = tid; i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
   if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
-  STATS_STAMP(6);
-#undef STATS_STAMP
 }
 
 // Otsu thresholds from the per-tile partial histograms a fused launch left in each view's
@@ -1049,18 +790,11 @@ __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (atomics only: see stats_kernel)
   __syncthreads();
   if (tid == 0) {
-    if (SLG_STATS_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t t = __hip_atomic_fetch_add(&ws->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *s_last = (t == uint32_t(n_blocks) - 1) ? 1u : 0u;
   }
   __syncthreads();
   if (!*s_last) return;
-  if (SLG_STATS_FENCE && tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
   for (int i = tid; act && i < 512; i += kBlock) {
     uint32_t acc = 0;
 #pragma unroll
@@ -1233,31 +967,12 @@ struct NoPre {
 // Constant counts make every frame load unconditional, so the decode consumes each pair as it
 // lands (vmcnt(n) in issue order) instead of after a vmcnt(0) for the whole batch, and drop the
 // per-pair branches (243.3 vs 259.8 us per 12-view launch, profiles/r3m).
-// One-view fused launches (SOLO): the thresholds come from the workgroups of the same launch
-// (solo_stats); a wave waits for them only once its frame loads are issued.
-__device__ inline void solo_wait(WsHeader* ws) {
-  // relaxed polls (an agent-scope acquire load invalidates the L2 on every poll: with ~4000
-  // waves polling that made the one-view launch 580 us, profiles/r5k)
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(&ws->solo[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-    __builtin_amdgcn_s_sleep(8);
-    // (cannot happen -- solo_stats always raises the flag; but a kernel must end: after 50 ms
-    // flag the error, bit 2, and go on; reconstruct_view refuses such a cloud)
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
-      atomicOr(&ws->error, 4u);
-      break;
-    }
-  }
-}
-
-template <int ROW_MODE, int SRC_FRAMES, int kBatch, bool MF = false, int PLAN = 0, class Pre = NoPre, bool SOLO = false>
+template <int ROW_MODE, int SRC_FRAMES, int kBatch, bool MF = false, int PLAN = 0, class Pre = NoPre>
 __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, uint32_t& valid,
                                    int (&col)[kPx], int (&row)[kPx], Pre pre = Pre()) {
   valid = 0;
   if (SRC_FRAMES) {
-    static_assert(!(SOLO && MF), "a one-view launch decodes densely: its mask waits for the thresholds");
-    int smin = 0, cmin = 0;
-    if constexpr (!SOLO) { smin = p.ws->smin; cmin = p.ws->cmin; }
+    const int smin = p.ws->smin, cmin = p.ws->cmin;
     const int64_t lp = px0 < p.n_px ? px0 : 0;
     const uint2 w = ld_frame8(p, 0, lp);
     const uint2 bl = ld_frame8(p, 1, lp);
@@ -1309,19 +1024,6 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
     uint32_t ac[4], ar[4];
     acc_codes(qc, np_c, p.col_pre, p.col_post, ac);
     acc_codes(qr, np_r, p.row_pre, p.row_post, ar);
-    if constexpr (SOLO) {                           // every frame load issued: now the thresholds
-      // one lane per workgroup polls (every wave polling put thousands of uncached loads a
-      // microsecond on the memory system: 170 us per one-view launch, profiles/r5l)
-      // what the thresholds' workgroup wrote and the waves read next -- smin, cmin, the zeroed
-      // look-back words -- is read by agent-scope atomics, so no cache invalidation is needed
-      SOLO_STAMP(2);
-      if (threadIdx.x == 0) solo_wait(p.ws);
-      __syncthreads();
-      SOLO_STAMP(3);
-      smin = __hip_atomic_load(&p.ws->smin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      cmin = __hip_atomic_load(&p.ws->cmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      pre(w);                                       // (a gray capture's colour: the white bytes)
-    }
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
       if constexpr (!MF) {
@@ -1599,81 +1301,6 @@ __device__ inline void publish_agg(uint64_t* w, int agg) {   // unless a helper 
 constexpr unsigned kNapCap = 8;         // back-off cap: 8 x s_sleep(2) ~ 1k clocks between re-polls
 constexpr unsigned kHelpAfter = 2048;   // s_sleep(2) units (~0.1 ms) before asking for help
 
-// Decoupled look-back over static tile ids (wave 0 calls it, lane 0 publishes).  Returns true
-// with the exclusive prefix of `agg` over the view's tiles before `tile`, or false with the
-// nearest predecessor that has not published for kHelpAfter (it may not be dispatched yet:
-// dispatch order is not guaranteed): the caller then computes that tile's aggregate itself
-// (tile_keep_count_wave) and retries, so waiting always ends.  Re-polls only the entries
-// newer than the nearest inclusive prefix, with capped back-off.
-template <bool PROF>
-__device__ bool lookback_try(const MainParams& p, uint64_t* st, int tile, int agg, uint64_t& excl_out,
-                             int& help_tile, uint32_t& polls, uint32_t& naps) {
-  const int lane = threadIdx.x & 63;
-  if (PROF && (p.dbg & 1)) { excl_out = uint64_t(tile) * kTilePx; return true; }   // ablation: no wait
-  if (tile == 0) {
-    if (lane == 0) st_state(&st[0], kFlagInc | uint64_t(agg));
-    excl_out = 0;
-    return true;
-  }
-  if (lane == 0) st_state(&st[tile], kFlagAgg | uint64_t(agg));   // a helper only ever writes this same value
-  const unsigned nap_cap = kNapCap;
-  const unsigned help_after = p.help_after;
-  uint64_t excl = 0;
-  int64_t j = tile - 1;
-  for (;;) {
-    ++polls;
-    uint64_t vv[kLookK];
-#pragma unroll
-    for (int k = 0; k < kLookK; ++k) {
-      const int64_t s = j - (k * 64 + lane);
-      vv[k] = s >= 0 ? ld_state(&st[s]) : kFlagInc;
-    }
-    unsigned slept = 0, nap = 1;
-    int pos;
-    for (;;) {
-      int my_pos = INT_MAX;
-#pragma unroll
-      for (int k = kLookK - 1; k >= 0; --k)
-        if ((vv[k] >> 62) == 2) my_pos = k * 64 + lane;
-      pos = wave_min_i(my_pos);
-      int my_miss = INT_MAX;                   // nearest unpublished entry newer than pos
-#pragma unroll
-      for (int k = kLookK - 1; k >= 0; --k)
-        if ((vv[k] >> 62) == 0 && k * 64 + lane <= pos) my_miss = k * 64 + lane;
-      const int miss = wave_min_i(my_miss);
-      if (miss == INT_MAX) break;
-      if (slept >= help_after) {
-        help_tile = int(j - miss);
-        return false;
-      }
-      for (unsigned z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(2);
-      slept += nap;
-      naps += nap;
-      ++polls;
-      nap = nap < nap_cap ? nap * 2 : nap_cap;
-#pragma unroll
-      for (int k = 0; k < kLookK; ++k) {
-        const int64_t s = j - (k * 64 + lane);
-        if ((vv[k] >> 62) == 0 && s >= 0 && k * 64 + lane <= pos) vv[k] = ld_state(&st[s]);
-      }
-    }
-    uint64_t sum = 0;
-#pragma unroll
-    for (int k = 0; k < kLookK; ++k)
-      if (k * 64 + lane <= pos) sum += vv[k] & kValMask;
-    excl += wave_sum(sum);
-    if (pos != INT_MAX) break;
-    j -= kLookK * 64;
-  }
-  if (lane == 0) st_state(&st[tile], kFlagInc | (excl + uint64_t(agg)));
-  excl_out = excl;
-  return true;
-}
-
-#ifndef SLG_SCALAR_LB
-#define SLG_SCALAR_LB 1                    // look-back polls through the scalar path (lookback_scalar)
-#endif
-
 // Look-back words st[b .. b+7] read by one scalar load that misses the scalar cache (glc): the
 // poll goes to L2 without queueing behind the co-resident workgroup's frame stream in the
 // CU's vector-memory pipeline (a vector poll waits behind up to ~180 KB of streaming loads).
@@ -1689,11 +1316,15 @@ __device__ inline void ld_state8_scalar(const uint64_t* p, uint64_t (&v)[8]) {
   for (int k = 0; k < 8; ++k) v[k] = uint64_t(r[2 * k]) | (uint64_t(r[2 * k + 1]) << 32);
 }
 
-// lookback_try's contract (same returns, same helper hand-off), polled 8 predecessors at a
-// time with wave-uniform scalar loads, newest first: aggregates are summed as they appear and
-// the walk stops at the first inclusive prefix; an unpublished entry is re-polled after a
-// capped back-off.  Published values never change (0 -> aggregate -> inclusive), so a stale
-// read only delays the walk, never changes the sum.
+// Decoupled look-back over static tile ids (wave 0 calls it, lane 0 publishes).  Returns true
+// with the exclusive prefix of `agg` over the view's tiles before `tile`, or false with the
+// nearest predecessor that has not published for p.help_after (it may not be dispatched yet:
+// dispatch order is not guaranteed): the caller then computes that tile's aggregate itself
+// (tile_keep_count_wave) and retries, so waiting always ends.  Polled 8 predecessors at a time
+// with wave-uniform scalar loads, newest first: aggregates are summed as they appear and the
+// walk stops at the first inclusive prefix; an unpublished entry is re-polled after a capped
+// back-off.  Published values never change (0 -> aggregate -> inclusive), so a stale read only
+// delays the walk, never changes the sum.
 template <bool PROF>
 __device__ bool lookback_scalar(const MainParams& p, uint64_t* st, int tile, int agg, uint64_t& excl_out,
                                 int& help_tile, uint32_t& polls, uint32_t& naps) {
@@ -1793,13 +1424,6 @@ constexpr int kMaxViews = 16;
 #ifndef SLG_TRI_GROUP
 #define SLG_TRI_GROUP 4                    // phase B: rounds (items per lane) whose gathers are in flight together
 #endif
-#ifndef SLG_TEX_LATE
-#define SLG_TEX_LATE 1                     // texture bytes read only by lanes with a valid pixel, after the
-                                           // decode (285.1 vs 289.7 us per 12-view launch, profiles/r3d/ab.log)
-#endif
-#ifndef SLG_MASK_FIRST
-#define SLG_MASK_FIRST 1                   // decode_lane MF: pattern frames read only where a pixel is valid
-#endif
 #ifndef SLG_M3_WAVES
 #define SLG_M3_WAVES 4                     // waves per SIMD main3 is register-budgeted for
 #endif
@@ -1838,7 +1462,7 @@ struct Main3Params {
   int32_t n_views;
   int32_t n_fin;              // views finished by this launch (FinIO), 0: none
   int32_t fin_blocks;         // finishing workgroups per such view (the grid's first n_fin*fin_blocks)
-  int32_t solo;               // one-view launch counting its own Otsu histograms (main3 SOLO)
+  int32_t pad_m3;
   int64_t n_state_words;      // look-back words per view slice (finishing arms them)
   int64_t pad_zero;           // zero bytes the last tile's partial counted past n_px
   ViewIO v[kMaxViews];
@@ -1967,73 +1591,9 @@ constexpr int kItemSlots = kTilePx + (kTilePx >> SLG_ITEM_PAD), kBgrSlots = kTil
 __device__ inline int item_slot(int m) { return m + (m >> SLG_ITEM_PAD); }
 __device__ inline int bgr_slot(int m) { return m + (m >> SLG_BGR_PAD); }
 
-#ifndef SLG_WB_PREFETCH
-#define SLG_WB_PREFETCH 0                  // white/black lines of the workgroup this far ahead, touched early
-#endif
-#ifndef SLG_D_HOIST
-#define SLG_D_HOIST 0                      // phase D: LDS reads hoisted, 32-bit offsets: 313.0 vs 312.0 us (r4q), off
-#endif
-#ifndef SLG_NT_STORES
-#define SLG_NT_STORES 0                    // phase D's XYZ / BGR stores non-temporal
-#endif
-#ifndef SLG_PRIO_A
-#define SLG_PRIO_A 0                       // s_setprio for phase A (decode: the frame stream) over B-D
-#endif
-template <typename T>
-__device__ inline void st_out(T* a, T v) {
-#if SLG_NT_STORES
-  __builtin_nontemporal_store(v, a);
-#else
-  *a = v;
-#endif
-}
-
-// Phase D's BGR output: 3 bytes per kept point, so a lane's own stores are a 2-byte and a 1-byte
-// store at odd addresses (16 per lane per tile).  Staged instead: each kept point's 24-bit colour
-// goes to LDS word l (its index within the tile's kept points), and the workgroup writes the
-// tile's contiguous byte range [3 base, 3 (base + agg)) as 16-byte aligned stores, each lane
-// packing six staged words into four output dwords; the two ragged end chunks go byte by byte.
 #ifndef SLG_X64_KEEP_T
 #define SLG_X64_KEEP_T 1                   // f64 XYZ, pinhole rays: t in registers, ray recomputed in phase D
 #endif
-#ifndef SLG_X64_STAGE
-#define SLG_X64_STAGE 0                    // f64 XYZ: per-wave LDS window, 16-byte aligned stores (r5a: 405.2
-#endif                                     // vs 405.9 us alone, 376.0 vs 364.2 with KEEP_T: off)
-#ifndef SLG_X64_PAIR
-#define SLG_X64_PAIR 0                     // f64 XYZ: (x, y) as one 16-byte store at 8-byte alignment + z
-#endif
-constexpr int kX64Window = 3 * 64 + 2;     // one round of a wave: 64 points + the alignment pad
-
-#ifndef SLG_BGR_STAGE
-#define SLG_BGR_STAGE 0                    // 329.3 vs 324.5 us per 16-view launch (profiles/r4j): off
-#endif
-constexpr int kStageWords = kTilePx + 8;          // + the 6-word read window past the last point
-
-__device__ inline void bgr_tile_store(uint8_t* gb, int64_t base, int agg, const uint32_t* w) {
-  const uint64_t start = reinterpret_cast<uint64_t>(gb) + uint64_t(3 * base);
-  const int a0 = int(start & 15u);
-  uint8_t* g = reinterpret_cast<uint8_t*>(start - uint64_t(a0));
-  const int nb = 3 * agg;                         // the tile's BGR bytes
-  const int nch = (a0 + nb + 15) >> 4;
-  for (int c = int(threadIdx.x); c < nch; c += kTileBlock) {
-    const int lo = c << 4, j0 = lo - a0;          // chunk start: in g, in the tile's byte stream
-    if (j0 >= 0 && j0 + 16 <= nb) {
-      const int l0 = j0 / 3, k0 = j0 - 3 * l0;
-      const uint32_t x0 = w[l0], x1 = w[l0 + 1], x2 = w[l0 + 2], x3 = w[l0 + 3], x4 = w[l0 + 4], x5 = w[l0 + 5];
-      const uint32_t q0 = x0 | (x1 << 24), q1 = (x1 >> 8) | (x2 << 16), q2 = (x2 >> 16) | (x3 << 8),
-                     q3 = x4 | (x5 << 24), q4 = x5 >> 8;   // the 18 stream bytes from point l0 on
-      const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(q1, q0, k0), __builtin_amdgcn_alignbyte(q2, q1, k0),
-                                 __builtin_amdgcn_alignbyte(q3, q2, k0), __builtin_amdgcn_alignbyte(q4, q3, k0));
-      *reinterpret_cast<uint4*>(g + lo) = v;
-    } else {
-      for (int t = 0; t < 16; ++t) {
-        const int j = j0 + t;
-        if (j >= 0 && j < nb) g[lo + t] = uint8_t(w[j / 3] >> (8 * (j % 3)));
-      }
-    }
-  }
-}
-
 // Phase B of main3 for rounds [i, i + G) (item m = tid + 256 * round), FAST path: the G items'
 // loads and fp64 chains are independent, so their plane gathers are in flight together.
 // tri_rounds: i is a compile-time multiple of G (the unrolled group loop); tri_rounds_at: any i.
@@ -2090,118 +1650,11 @@ __device__ inline void tri_rounds(const MainParams& p, int i, int n_items, const
   tri_rounds_at<G, ROW_MODE, RAYS, XT, NS, kIt, NP, NC>(p, i, n_items, s_item, pts, km);
 }
 
-// The Otsu stats of a one-view fused launch (SOLO), done by the launch's own workgroups before
-// their tiles: each claims 4096-pixel chunks of the view (ws->solo[0]) until none is left,
-// histograms a chunk on the matrix cores (the carried-histogram code, hist_next_*), adds it to
-// the view's histogram copies and takes a ticket (ws->solo[1]); the workgroup counting the last
-// chunk sums the copies, runs Otsu (otsu_wave, as stats_kernel), arms the look-back words and
-// raises ws->solo[3].  No workgroup waits before it has claimed past the last chunk, and every
-// claimed chunk belongs to a running workgroup that waits for nothing, so the flag always comes:
-// whatever order the workgroups are dispatched in, the launch cannot deadlock.
-__device__ __attribute__((always_inline)) inline void solo_stats(const MainParams& p, int64_t n_tiles,
-                                                                 int64_t n_state_words, int64_t pad_zero,
-                                                                 uint2* s_hstage, uint32_t* s_hn, uint32_t* s_lds,
-                                                                 int* s_flag) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  WsHeader* ws = p.ws;
-  uint32_t* hist_part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + kHistPartOff);
-  // (claiming the next chunk while counting this one made a few workgroups take two chunks
-  // each and the last ticket come later: 34 vs 25 us, profiles/r5o)
-  for (;;) {
-    if (tid == 0) *s_flag = int(atomicAdd(&ws->solo[0], 1u));
-    __syncthreads();
-    const int64_t c = *s_flag;
-    __syncthreads();
-    if (c >= n_tiles) break;
-    const int64_t o = c * kTilePx + int64_t(tid) * kPx;
-    uint2 wq, bq;
-    hist_next_load(p.frames, p.frames + p.stride, p.n_px, o, wq, bq);
-    for (int i = tid; i < 512; i += kTileBlock) s_hn[i] = 0;
-    hist_next_stage(wq, bq, p.n_px, o, s_hstage);
-    __syncthreads();
-    hist_next_count(s_hstage, s_hn, wave, kTileBlock / 64);
-    __syncthreads();
-    for (int i = tid; i < 512; i += kTileBlock) {
-      const uint32_t v = s_hn[i];
-      if (v) atomicAdd(hist_part + (c % kHistCopies) * 512 + i, v);
-    }
-    // the chunk's counts are agent-scope atomics: complete (vmcnt) before the ticket, no L2
-    // write-back (an agent-scope release fence is a buffer_wbl2 of the whole L2: one per
-    // workgroup and chunk made the one-view launch ~160 us, profiles/r5l)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const uint32_t d = __hip_atomic_fetch_add(&ws->solo[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *s_flag = d == uint32_t(n_tiles - 1) ? 1 : 0;
-    }
-    __syncthreads();
-    if (*s_flag) {                                   // the last chunk: thresholds for the launch
-      SOLO_STAMP(6);
-      if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __syncthreads();
-      uint32_t* hg = s_lds;
-      for (int i = tid; i < 512; i += kTileBlock) {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int k = 0; k < kHistCopies; ++k)
-          acc += __hip_atomic_load(hist_part + k * 512 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((i & 255) == 0) acc -= uint32_t(pad_zero);   // zero bytes staged past n_px
-        hg[i] = acc;
-      }
-      __syncthreads();
-      if (wave < 2) {                                // wave 0: white, wave 1: clip(w-b)
-        const double thr = otsu_wave(hg + 256 * wave, p.n_px, reinterpret_cast<double*>(s_lds + 512) + wave * kOtsuLds);
-        const int m = int_threshold(thr, wave == 0 ? 0 : -255);
-        const int64_t above = hist_at_least_wave(hg + 256 * wave, m, p.n_px);
-        if (lane == 0) {
-          if (wave == 0) {
-            __hip_atomic_store(&ws->smin, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ws->thr_s = thr;
-          } else {
-            __hip_atomic_store(&ws->cmin, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ws->thr_c = thr;
-          }
-          ws->above[wave] = above;
-        }
-      } else {                                       // the other waves meanwhile: arm the look-back,
-        static_assert(kTileBlock > 128, "the resets need waves beside the two Otsu waves");
-        const int t = tid - 128;                     // reset the histogram copies
-        uint64_t* states = p.states;
-        for (int64_t i = t; i < n_state_words; i += kTileBlock - 128) states[i] = 0;
-        for (int i = t; i < kHistCopies * 512; i += kTileBlock - 128) hist_part[i] = 0;
-        if (t == 0) { ws->solo[1] = 0; ws->tile_counter = 0; }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_store(&ws->solo[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      SOLO_STAMP(7);
-    }
-    __syncthreads();
-  }
-}
-
-// The last workgroup of a one-view fused launch to leave resets the SOLO words for the next one
-// (atomics only: every workgroup's uses of them are atomics, done before its exit ticket).
-__device__ inline void solo_exit(WsHeader* ws, int n_wg) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t e = __hip_atomic_fetch_add(&ws->solo[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (e == uint32_t(n_wg - 1)) {
-      __hip_atomic_store(&ws->solo[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ws->solo[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ws->solo[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 // PROF: the profiling instance (SLG_DBG set): honours the ablation bits of MainParams::dbg and
 // writes per-workgroup phase records; the production instances carry none of that code.
 constexpr int kPlanGray = 0x100;           // PLAN bit: every view of the launch is a gray capture
 
-template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS, bool PROF, int PLAN = 0, bool SOLO = false>
+template <int ROW_MODE, int XYZ64, int SRC_FRAMES, int RAYS, bool PROF, int PLAN = 0>
 __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAVES) void main3_kernel(Main3Params P) {
   using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
   constexpr int NS = ROW_MODE == 2 ? 2 : 1;
@@ -2211,18 +1664,12 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   __shared__ uint32_t s_bgr[kBgrSlots];    // its BGR (24 bits)
   __shared__ int s_wtot[kB / 64];
   __shared__ int s_cnt[NS][kIt][kB / 64];  // kept points per (round, wave)
-#if SLG_D_HOIST
-  __shared__ __attribute__((aligned(16))) int s_loc[NS][kB / 64][kIt];   // (wave-major: one wave's 8 in a row)
-#else
   __shared__ int s_loc[NS][kIt][kB / 64];  // their exclusive offsets within the tile (phase C)
-#endif
   __shared__ uint64_t s_excl[NS];
-  __shared__ int s_agg[NS];                // kept points of the tile (phase C)
   // the carried batch's nibble planes and histograms in LDS of their own (68 KB per workgroup,
   // two per CU): each wave stages its lane data as soon as phase A ends, no extra barrier
   // (289.7 vs 291.6 us per launch against aliasing the item arrays after phase B)
   __shared__ __attribute__((aligned(16))) uint2 s_hstage[(kB / 64) * 256];   // [wave][4 planes][64 lanes]
-  static_assert(kX64Window * 8 <= 256 * 8, "phase D's per-wave f64 window fits the wave's staging");
   __shared__ uint32_t s_hn[512];                                      // histograms
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2249,14 +1696,6 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // look-back, D stores (100 MHz ticks), look-back polls, sleep units, items, start} written to
   // view 0's partials region (tools/kbench.py "phases"; the host refuses it when a batch is
   // carried, whose partials live there).
-  if constexpr (SOLO) {                              // the view's thresholds, counted right here
-    SOLO_STAMP(0);
-#if SLG_SOLO_PROF
-    if (tid == 0 && blockIdx.x < 1024) { g_solo_rec[blockIdx.x * 8 + 6] = 0; g_solo_rec[blockIdx.x * 8 + 7] = 0; }
-#endif
-    solo_stats(p, tiles, P.n_state_words, P.pad_zero, s_hstage, s_hn, reinterpret_cast<uint32_t*>(s_item), &s_wtot[0]);
-    SOLO_STAMP(1);
-  }
   const bool prof = PROF && (p.dbg & 64) != 0;
   uint64_t t_phase = prof ? __builtin_amdgcn_s_memrealtime() : 0;
   // the record lives in LDS (tid 0 writes it): as a register array it pushed the profiling
@@ -2272,23 +1711,6 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     }
   };
 
-  // SLG_WB_PREFETCH = D > 0: also touch the white / black lines of the workgroup D places later
-  // in dispatch order (one 4-byte load per lane and frame, issued beside this tile's own), so
-  // they are in the Infinity Cache when that workgroup starts: its first round trip (the mask
-  // loads) then hits on chip.  The values are folded into a sink after phase A (no wait before).
-  uint32_t pf_a = 0, pf_b = 0;
-  if (SLG_WB_PREFETCH > 0 && SRC_FRAMES) {
-    const int tb = bid + SLG_WB_PREFETCH;
-    if (tb < tiles * P.n_views) {                    // block-uniform
-      const int t2 = tb / P.n_views, v2 = tb - t2 * P.n_views;
-      const int64_t q0 = int64_t(t2) * kTilePx + int64_t(tid) * kPx;
-      const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(P.v[v2].frames), 0,
-                                                                          0xffffffff, 0x00020000);
-      const uint32_t o2 = uint32_t(q0 < P.c.n_px ? q0 : 0);
-      pf_a = __builtin_amdgcn_raw_buffer_load_b32(r2, o2, 0, 0);
-      pf_b = __builtin_amdgcn_raw_buffer_load_b32(r2, o2, uint32_t(P.v[v2].stride), 0);
-    }
-  }
   // stats pass of the batch after next (hist_next_*): loads now, counting during phase C
   const bool hn = P.v[view].hn_part != nullptr;     // block-uniform
   uint2 hn_w, hn_b;
@@ -2297,7 +1719,6 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   }
   // ------------------------------------------------------------ A: decode + tile compaction
   int n_items;
-  if (SLG_PRIO_A) __builtin_amdgcn_s_setprio(SLG_PRIO_A);
   {
     uint32_t tex[6] = {0, 0, 0, 0, 0, 0};
     // texture NULL: a gray capture, whose cv2.imread(files[0]) is frame 0 replicated -- the white
@@ -2320,25 +1741,17 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
           if (px0 * 3 + k < p.n_px * 3) tex[k >> 2] |= uint32_t(p.texture[px0 * 3 + k]) << (8 * (k & 3));
       }
     };
-    constexpr bool MF = SLG_MASK_FIRST && SRC_FRAMES && !SOLO;
-    if (!SLG_TEX_LATE && !MF && !(SOLO && gray)) load_tex(make_uint2(0u, 0u));   // (gray: MF or SOLO)
     uint32_t valid;
     int col[kPx], row[kPx];
-    if constexpr (SOLO) {
-      // one view: every frame read densely while the thresholds are being counted; a gray
-      // capture's colour comes from the white bytes once they are known to be needed
-      auto pre_gray = [&](uint2 w) { if (gray) load_tex(w); };
-      decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH, false, PLAN, decltype(pre_gray), true>(p, px0, tail, valid, col,
-                                                                                             row, pre_gray);
-    } else if constexpr (MF) {
+    if constexpr (SRC_FRAMES) {
       // mask first: a lane with a valid pixel issues its texture loads, then its pattern loads
       decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH, true, PLAN>(p, px0, tail, valid, col, row, load_tex);
     } else {
+      // maps source (slg_triangulate): only lanes with a valid pixel read their 24 texture
+      // bytes, once the mask is known (the block scan's barrier covers part of the latency)
       decode_lane<ROW_MODE, SRC_FRAMES, SLG_DECODE_BATCH, false, PLAN>(p, px0, tail, valid, col, row);
+      if (valid != 0u) load_tex(make_uint2(0u, 0u));
     }
-    // SLG_TEX_LATE: only lanes with a valid pixel read their 24 texture bytes, once the mask is
-    // known (the block scan's barrier covers part of the latency)
-    if (!MF && SLG_TEX_LATE && valid != 0u && !(SOLO && gray)) load_tex(make_uint2(0u, 0u));
     const int2 sc = block_scan(__popc(valid), s_wtot);
     n_items = sc.y;
     int m = sc.x;
@@ -2355,10 +1768,6 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     }
   }
   __syncthreads();
-  if constexpr (SOLO) SOLO_STAMP(4);
-  if (SLG_PRIO_A) __builtin_amdgcn_s_setprio(0);
-  if (SLG_WB_PREFETCH > 0 && (pf_a ^ pf_b) == 0x9e3779b9u && p.dbg == 0x7fffffff)
-    atomicOr(&p.ws->error, 0u);                      // (never: keeps the prefetch loads)
 
   stamp(0);
   if (hn) {                                          // block-uniform; counted in phase C
@@ -2476,16 +1885,12 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
         const int y = __shfl_up(incl, o);
         if (lane >= o) incl += y;
       }
-      if (lane < kEnt) {
-        if (SLG_D_HOIST) (&s_loc[s][0][0])[(lane % (kB / 64)) * kIt + lane / (kB / 64)] = incl - cnt;
-        else (&s_loc[s][0][0])[lane] = incl - cnt;
-      }
+      if (lane < kEnt) (&s_loc[s][0][0])[lane] = incl - cnt;
       const int agg = __shfl(incl, 63);
       uint64_t* st = p.states + int64_t(s) * tiles;
       uint64_t excl;
       int ht;
-      while (!(SLG_SCALAR_LB ? lookback_scalar<PROF>(p, st, tile, agg, excl, ht, polls, naps)
-                             : lookback_try<PROF>(p, st, tile, agg, excl, ht, polls, naps))) {
+      while (!lookback_scalar<PROF>(p, st, tile, agg, excl, ht, polls, naps)) {
         // a predecessor has not published for long (it may not be dispatched yet): publish
         // its aggregate for it, computed by this wave, and look back again
         const int hagg = tile_keep_count_wave<ROW_MODE, SRC_FRAMES, RAYS>(p, ht, s);
@@ -2496,7 +1901,6 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       }
       if (lane == 0) {
         s_excl[s] = excl;
-        s_agg[s] = agg;
         if (tail) {
           p.ws->totals[s] = int64_t(excl) + agg;
           if (ROW_MODE != 2) *p.count = int64_t(excl) + agg;
@@ -2513,41 +1917,6 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // ------------------------------------------------------------ D: ordered stores from registers
   if (PROF && (p.dbg & 4)) return;                   // ablation: no output stores
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  // BGR staging words (SLG_BGR_STAGE) alias the item array: its last reader was phase B
-  static_assert(NS * kStageWords * 4 <= kItemSlots * 8, "BGR staging fits the item array");
-  uint32_t* s_stage = reinterpret_cast<uint32_t*>(s_item);
-#if SLG_D_HOIST
-  // every LDS read of the phase first (the rounds' offsets, one wave-uniform row; their colours),
-  // then the stores: one LDS wait instead of one per round, and 32-bit offsets from the tile's
-  // uniform base pointers
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int64_t base = int64_t(s_excl[s]);
-    XT* gx = reinterpret_cast<XT*>(s == 0 ? p.xyz : p.scratch_xyz) + 3 * base;
-    uint8_t* gb = (s == 0 ? p.bgr : p.scratch_bgr) + 3 * base;
-    int loc[kIt];
-    uint32_t col[kIt];
-#pragma unroll
-    for (int i = 0; i < kIt; ++i) {
-      loc[i] = s_loc[s][wave][i];
-      col[i] = s_bgr[bgr_slot(tid + kB * i)];
-    }
-#pragma unroll
-    for (int i = 0; i < kIt; ++i) {
-      if ((km[s][i] >> lane) & 1ull) {
-        const uint32_t l = uint32_t(loc[i] + __popcll(km[s][i] & lt));
-        const uint32_t c = col[i];
-        if (!(PROF && (p.dbg & 128))) {
-          st_out(gx + 3 * l, pts[s][i][0]); st_out(gx + 3 * l + 1, pts[s][i][1]); st_out(gx + 3 * l + 2, pts[s][i][2]);
-        }
-        if (!(PROF && (p.dbg & 8))) {
-          st_out(gb + 3 * l, uint8_t(c)); st_out(gb + 3 * l + 1, uint8_t(c >> 8)); st_out(gb + 3 * l + 2, uint8_t(c >> 16));
-        }
-      }
-    }
-  }
-  if (false)
-#endif
   // the point of round i, stream s: from registers, or (KT) Oc + r * t with the ray recomputed
   auto point_of = [&](int s, int i, XT& x, XT& y, XT& z) {
     if constexpr (KT) {
@@ -2561,13 +1930,9 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       x = pts[s][i][0]; y = pts[s][i][NC - 1 < 1 ? 0 : 1]; z = pts[s][i][NC - 1];
     }
   };
-  // f64 XYZ through a per-wave LDS window (SLG_X64_STAGE, off: measured no faster): a wave's kept points of one round are
-  // one contiguous run of the cloud, written as 16-byte aligned stores -- 24 bytes per point in
-  // 1.5 stores and whole lines, where each lane's three 8-byte stores at a 24-byte stride touch
-  // 12 lines per instruction.  No workgroup barrier: the window is the wave's own (the carried
-  // histogram staging, free once phase C's barrier has passed).
-  constexpr bool XS = XYZ64 && SLG_X64_STAGE;
-  double* s_xw = reinterpret_cast<double*>(s_hstage) + wave * kX64Window;
+  // (tried and measured no faster, in git history: BGR staged through LDS as 16-byte stores,
+  // phase D's LDS reads hoisted, non-temporal stores, f64 XYZ through a per-wave LDS window or
+  // as 16 + 8-byte stores -- DESIGN.md §4)
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int64_t base = int64_t(s_excl[s]);
@@ -2575,67 +1940,20 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     uint8_t* gb = s == 0 ? p.bgr : p.scratch_bgr;
 #pragma unroll
     for (int i = 0; i < kIt; ++i) {
-      if (XS && km[s][i] != 0ull && !(PROF && (p.dbg & 128))) {      // wave-uniform
-        const int64_t q0 = base + s_loc[s][i][wave];                   // the wave's first point
-        const int n = __popcll(km[s][i]);
-        // a = 1: the run starts in the middle of a 16-byte pair; window slot 0 is then a pad
-        const int a = int(((reinterpret_cast<uintptr_t>(gx) >> 3) + 3 * uint64_t(q0)) & 1u);
-        if ((km[s][i] >> lane) & 1ull) {
-          XT x, y, z;
-          point_of(s, i, x, y, z);
-          const int w = 3 * __popcll(km[s][i] & lt) + a;
-          s_xw[w] = double(x); s_xw[w + 1] = double(y); s_xw[w + 2] = double(z);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int nd = 3 * n + a;                                     // window doubles incl. the pad
-        double* g = reinterpret_cast<double*>(gx) + 3 * q0 - a;       // 16-byte aligned
-        for (int d0 = 2 * lane; d0 < nd; d0 += 128) {
-          if (d0 >= a && d0 + 1 < nd) {
-            st_out(reinterpret_cast<double2*>(g + d0), *reinterpret_cast<const double2*>(s_xw + d0));
-          } else {
-            if (d0 >= a) st_out(g + d0, s_xw[d0]);
-            if (d0 + 1 < nd) st_out(g + d0 + 1, s_xw[d0 + 1]);
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");       // reads done before the next round's writes
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
       if ((km[s][i] >> lane) & 1ull) {
         const int l = s_loc[s][i][wave] + __popcll(km[s][i] & lt);
         const int64_t q = base + l;
         const uint32_t c = s_bgr[bgr_slot(tid + kB * i)];
-        if (!XS && !(PROF && (p.dbg & 128))) {       // PROF ablation bit 7: no XYZ stores
+        if (!(PROF && (p.dbg & 128))) {              // PROF ablation bit 7: no XYZ stores
           XT x, y, z;
           point_of(s, i, x, y, z);
-          if constexpr (XYZ64 && SLG_X64_PAIR) {
-            typedef double d2a8 __attribute__((ext_vector_type(2), aligned(8)));
-            *reinterpret_cast<d2a8*>(gx + 3 * q) = d2a8{double(x), double(y)};
-            st_out(gx + 3 * q + 2, z);
-          } else {
-            st_out(gx + 3 * q, x); st_out(gx + 3 * q + 1, y); st_out(gx + 3 * q + 2, z);
-          }
+          gx[3 * q] = x; gx[3 * q + 1] = y; gx[3 * q + 2] = z;
         }
-        if (SLG_BGR_STAGE) {
-          s_stage[s * kStageWords + l] = c;
-        } else if (!(PROF && (p.dbg & 8))) {         // PROF ablation bit 3: no BGR stores
-          st_out(gb + 3 * q, uint8_t(c)); st_out(gb + 3 * q + 1, uint8_t(c >> 8)); st_out(gb + 3 * q + 2, uint8_t(c >> 16));
+        if (!(PROF && (p.dbg & 8))) {                // PROF ablation bit 3: no BGR stores
+          gb[3 * q] = uint8_t(c); gb[3 * q + 1] = uint8_t(c >> 8); gb[3 * q + 2] = uint8_t(c >> 16);
         }
       }
     }
-  }
-  if (SLG_BGR_STAGE) {
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      if (!(PROF && (p.dbg & 8)))
-        bgr_tile_store(s == 0 ? p.bgr : p.scratch_bgr, int64_t(s_excl[s]), s_agg[s], s_stage + s * kStageWords);
-  }
-  if constexpr (SOLO) {
-    solo_exit(p.ws, int(gridDim.x));
-    SOLO_STAMP(5);
   }
   if (prof) {
     __syncthreads();
@@ -2838,14 +2156,13 @@ int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* black
   sp.thresh_mode = dp ? dp->thresh_mode : SLG_THRESH_MANUAL;
   sp.shadow_val = dp ? dp->shadow_val : 0.0;
   sp.contrast_val = dp ? dp->contrast_val : 0.0;
-  sp.dbg = debug_flags();
   // Few fat workgroups per view: each merges its sub-histograms into the view's histogram with
   // <= 512 global atomics, and a batch's stats pass takes few CU slots next to a fused launch.
-  // One-view Otsu launches: kOtsuSoloChunks MFMA chunks per wave.
-  const bool otsu_solo = n_views == 1 && sp.thresh_mode == SLG_THRESH_OTSU;
-  const int64_t px_per_block = otsu_solo ? int64_t(kBlock / 64) * kHistChunk * kOtsuSoloChunks : int64_t(kBlock) * kStatsPx;
+  // One-view Otsu launches: kOtsuOneChunks MFMA chunks per wave.
+  const bool otsu_one = n_views == 1 && sp.thresh_mode == SLG_THRESH_OTSU;
+  const int64_t px_per_block = otsu_one ? int64_t(kBlock / 64) * kHistChunk * kOtsuOneChunks : int64_t(kBlock) * kStatsPx;
   int64_t grid = (n_px + px_per_block - 1) / px_per_block;
-  const int64_t cap = otsu_solo ? 4 * kStatsBlocksSolo : n_views == 1 ? kStatsBlocksSolo
+  const int64_t cap = otsu_one ? 4 * kStatsBlocksOne : n_views == 1 ? kStatsBlocksOne
                     : sp.thresh_mode == SLG_THRESH_OTSU ? kStatsBlocksOtsu : kStatsBlocks;
   if (grid > cap) grid = cap;
   if (sp.thresh_mode == SLG_THRESH_OTSU) {   // bound chunks per wave (i32 MFMA accumulators)
@@ -2947,11 +2264,11 @@ uint32_t help_after() {   // look-back helper delay; SLG_HELP_AFTER=0 forces the
 
 using Main3Fn = void (*)(Main3Params);
 
-// Production instances for every (row_mode, xyz, source, ray) case; the profiling instance
+// Production instances for every (source, row_mode, xyz, ray) case; the profiling instance
 // (SLG_DBG with any main3 bit) exists for the benchmark shape only: row_mode 1, f32 XYZ, frames,
 // pinhole rays (tools/kbench.py).
 // Decode plans main3 has specialised instances for (PLAN = (col_pairs << 4) | row_pairs), with
-// row_mode 1 or 2 and pinhole rays: C2's 11 + 10 bits (1920x1080 projector, row_scale 2), the
+// row_mode 1 and pinhole rays: C2's 11 + 10 bits (1920x1080 projector, row_scale 2), the
 // reference's default 11 + 11 (processing.py:29-30; C3, C5) and C4's 12 + 12; row_mode 0: C1's
 // 10 column bits.
 #define SLG_PLAN_C2 0xBA
@@ -2959,50 +2276,143 @@ using Main3Fn = void (*)(Main3Params);
 #define SLG_PLAN_C4 0xCC
 #define SLG_PLAN_C1 0xA0           // row_mode 0, 10 column bits (1024-wide projector), no row pairs
 
-template <int SRC>
-Main3Fn pick_main(int row_mode, int x64, int rays, int plan = 0, bool solo = false) {
-#ifndef SLG_FAST_BUILD
-  if (SRC == 1 && solo && !(debug_flags() & kMainDbgBits)) {   // one-view launches with in-launch stats
-#define SLG_SCASE(RM, X, R) if (row_mode == RM && x64 == X && rays == R) return main3_kernel<RM, X, 1, R, false, 0, true>;
-    SLG_SCASE(0, 0, 0) SLG_SCASE(0, 0, 1) SLG_SCASE(0, 1, 0) SLG_SCASE(0, 1, 1)
-    SLG_SCASE(1, 0, 0) SLG_SCASE(1, 0, 1) SLG_SCASE(1, 1, 0) SLG_SCASE(1, 1, 1)
-    SLG_SCASE(2, 0, 0) SLG_SCASE(2, 0, 1) SLG_SCASE(2, 1, 0) SLG_SCASE(2, 1, 1)
-#undef SLG_SCASE
+// Every main3 instance the library can launch, one table: pick_main only returns pointers from
+// it, and only those whose device code is in the library's gfx950 code object
+// (device_symbols): the HIP runtime aborts the process on a launch -- or any query -- of a kernel
+// whose code object lacks it (a round-5 run ended that way: DESIGN.md §4), so a missing
+// instance must be caught before the runtime sees it.
+struct Main3Inst {
+  int src, row_mode, x64, rays, plan;
+  bool prof;
+  Main3Fn fn;
+};
+#define SLG_M3(S, RM, X, R, P, PL) {S, RM, X, R, PL, P, main3_kernel<RM, X, S, R, P, PL>},
+#define SLG_M3_GENERIC(S)                                                                          \
+  SLG_M3(S, 0, 0, 0, false, 0) SLG_M3(S, 0, 0, 1, false, 0) SLG_M3(S, 0, 1, 0, false, 0)          \
+  SLG_M3(S, 0, 1, 1, false, 0) SLG_M3(S, 1, 0, 0, false, 0) SLG_M3(S, 1, 0, 1, false, 0)          \
+  SLG_M3(S, 1, 1, 0, false, 0) SLG_M3(S, 1, 1, 1, false, 0) SLG_M3(S, 2, 0, 0, false, 0)          \
+  SLG_M3(S, 2, 0, 1, false, 0) SLG_M3(S, 2, 1, 0, false, 0) SLG_M3(S, 2, 1, 1, false, 0)
+#define SLG_M3_PLAN(RM, PL) SLG_M3(1, RM, 0, 1, false, PL) SLG_M3(1, RM, 1, 1, false, PL)         \
+  SLG_M3(1, RM, 0, 1, false, (PL) | kPlanGray) SLG_M3(1, RM, 1, 1, false, (PL) | kPlanGray)
+const Main3Inst kMain3Table[] = {
+#ifdef SLG_FAST_BUILD   // register/spill inspection builds only: the benchmark's instances alone
+    SLG_M3(1, 1, 0, 1, false, SLG_PLAN_C2) SLG_M3(1, 1, 0, 1, false, 0)
+#else
+    SLG_M3_GENERIC(0) SLG_M3_GENERIC(1)
+    SLG_M3_PLAN(1, SLG_PLAN_C2) SLG_M3_PLAN(1, SLG_PLAN_1080P) SLG_M3_PLAN(1, SLG_PLAN_C4)
+    SLG_M3_PLAN(0, SLG_PLAN_C1)
+    SLG_M3(1, 1, 0, 1, true, SLG_PLAN_C2) SLG_M3(1, 1, 0, 1, true, 0)
+#endif
+};
+#undef SLG_M3_PLAN
+#undef SLG_M3_GENERIC
+#undef SLG_M3
+
+// Itanium name of main3_kernel<RM, X, S, R, P, PL> (anonymous namespace), as the code object and
+// the runtime's registration spell it.
+std::string main3_symbol(const Main3Inst& k) {
+  auto li = [](int v) { return "Li" + (v < 0 ? "n" + std::to_string(-v) : std::to_string(v)) + "E"; };
+  return "_ZN12_GLOBAL__N_112main3_kernelI" + li(k.row_mode) + li(k.x64) + li(k.src) + li(k.rays) +
+         std::string(k.prof ? "Lb1E" : "Lb0E") + li(k.plan) + "EEvNS_11Main3ParamsE";
+}
+
+// Symbol names of this library's gfx950 code objects: the clang offload bundles in its own file
+// (found by dladdr), each gfx950 entry an ELF whose symbol tables are read.  File reads only --
+// no HIP call, so nothing here can trip the runtime's abort.  Empty when the file cannot be read.
+const std::vector<std::string>& device_symbols() {
+  static std::vector<std::string> names;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    Dl_info info{};
+    if (!dladdr(reinterpret_cast<void*>(&slg_version), &info) || !info.dli_fname) return;
+    FILE* f = fopen(info.dli_fname, "rb");
+    if (!f) return;
+    std::vector<uint8_t> b;
+    if (fseek(f, 0, SEEK_END) == 0) {
+      const long n = ftell(f);
+      if (n > 0 && fseek(f, 0, SEEK_SET) == 0) {
+        b.resize(size_t(n));
+        if (fread(b.data(), 1, b.size(), f) != b.size()) b.clear();
+      }
+    }
+    fclose(f);
+    auto u16 = [&](size_t o) { uint16_t v; memcpy(&v, &b[o], 2); return v; };
+    auto u32 = [&](size_t o) { uint32_t v; memcpy(&v, &b[o], 4); return v; };
+    auto u64 = [&](size_t o) { uint64_t v; memcpy(&v, &b[o], 8); return v; };
+    static const char kMagic[] = "__CLANG_OFFLOAD_BUNDLE__";
+    const size_t ml = sizeof(kMagic) - 1;
+    for (size_t at = 0; at + ml + 8 <= b.size(); ++at) {
+      if (b[at] != '_' || memcmp(&b[at], kMagic, ml) != 0) continue;
+      size_t e = at + ml;
+      const uint64_t n_ent = u64(e);
+      e += 8;
+      for (uint64_t k = 0; k < n_ent && e + 24 <= b.size(); ++k) {
+        const uint64_t off = u64(e), size = u64(e + 8), tl = u64(e + 16);
+        e += 24;
+        if (e + tl > b.size()) break;
+        const std::string triple(reinterpret_cast<const char*>(&b[e]), size_t(tl));
+        e += tl;
+        const size_t o = at + off;                 // the entry: an ELF64 code object
+        if (triple.find("gfx950") == std::string::npos || o + 64 > b.size() || off + size > b.size() - at ||
+            memcmp(&b[o], "\x7f" "ELF", 4) != 0)
+          continue;
+        const uint64_t shoff = u64(o + 0x28);
+        const uint16_t shentsize = u16(o + 0x3a), shnum = u16(o + 0x3c);
+        if (shentsize < 64 || o + shoff + uint64_t(shnum) * shentsize > b.size()) continue;
+        for (uint16_t si = 0; si < shnum; ++si) {
+          const size_t sh = o + shoff + size_t(si) * shentsize;
+          const uint32_t type = u32(sh + 4);
+          if (type != 2 && type != 11) continue;   // SHT_SYMTAB, SHT_DYNSYM
+          const uint64_t sym_off = u64(sh + 24), sym_size = u64(sh + 32), ent = u64(sh + 56);
+          const uint32_t link = u32(sh + 40);
+          if (ent < 24 || link >= shnum) continue;
+          const size_t strh = o + shoff + size_t(link) * shentsize;
+          const uint64_t str_off = u64(strh + 24), str_size = u64(strh + 32);
+          if (o + sym_off + sym_size > b.size() || o + str_off + str_size > b.size()) continue;
+          for (uint64_t q = 0; q + ent <= sym_size; q += ent) {
+            const uint32_t nm = u32(o + sym_off + q);
+            if (nm == 0 || nm >= str_size) continue;
+            const char* c = reinterpret_cast<const char*>(&b[o + str_off + nm]);
+            names.emplace_back(c, strnlen(c, size_t(str_size - nm)));
+          }
+        }
+      }
+    }
+    std::sort(names.begin(), names.end());
+  });
+  return names;
+}
+
+bool device_has(const std::string& name) {
+  const auto& v = device_symbols();
+  return std::binary_search(v.begin(), v.end(), name);
+}
+
+// The kernel of a (source, row_mode, xyz, rays, plan) launch: the plan's specialised instance
+// if the table has one, else the generic one; the profiling instance when SLG_DBG asks for it.
+// NULL (and *why set) when the table has none or its device code is missing.
+Main3Fn pick_main(int src, int row_mode, int x64, int rays, int plan, const char** why) {
+  const bool prof = (debug_flags() & kMainDbgBits) != 0;
+  const Main3Inst* hit = nullptr;
+  for (int pass = 0; pass < 2 && !hit; ++pass) {
+    const int want = pass == 0 ? plan : 0;
+    if (pass == 1 && plan == 0) break;
+    for (const Main3Inst& k : kMain3Table)
+      if (k.src == src && k.row_mode == row_mode && k.x64 == x64 && k.rays == rays && k.plan == want && k.prof == prof) {
+        hit = &k;
+        break;
+      }
+  }
+  if (!hit) {
+    *why = prof ? "no kernel for this configuration (SLG_DBG profiling: row_mode 1, f32, frames, pinhole only)"
+                : "no kernel for this configuration";
     return nullptr;
   }
-#endif
-  if (debug_flags() & kMainDbgBits) {
-    if (!(SRC == 1 && row_mode == 1 && x64 == 0 && rays == SLG_RAYS_PINHOLE)) return nullptr;
-    return plan == SLG_PLAN_C2 ? main3_kernel<1, 0, 1, 1, true, SLG_PLAN_C2> : main3_kernel<1, 0, 1, 1, true>;
+  if (!device_has(main3_symbol(*hit))) {
+    *why = "the library's code object lacks this kernel instance (rebuild libslgpu.so)";
+    return nullptr;
   }
-#ifndef SLG_FAST_BUILD
-  if (SRC == 1 && rays == SLG_RAYS_PINHOLE && row_mode != 0) {
-#define SLG_PCASE(RM, X, PL) if (row_mode == RM && x64 == X && plan == (PL)) return main3_kernel<RM, X, 1, 1, false, (PL)>;
-    SLG_PCASE(1, 0, SLG_PLAN_C2) SLG_PCASE(1, 1, SLG_PLAN_C2)
-    SLG_PCASE(1, 0, SLG_PLAN_1080P) SLG_PCASE(1, 1, SLG_PLAN_1080P)
-    SLG_PCASE(1, 0, SLG_PLAN_C4) SLG_PCASE(1, 1, SLG_PLAN_C4)
-    SLG_PCASE(1, 0, SLG_PLAN_C2 | kPlanGray) SLG_PCASE(1, 1, SLG_PLAN_C2 | kPlanGray)
-    SLG_PCASE(1, 0, SLG_PLAN_1080P | kPlanGray) SLG_PCASE(1, 1, SLG_PLAN_1080P | kPlanGray)
-    SLG_PCASE(1, 0, SLG_PLAN_C4 | kPlanGray) SLG_PCASE(1, 1, SLG_PLAN_C4 | kPlanGray)
-  }
-  if (SRC == 1 && rays == SLG_RAYS_PINHOLE && row_mode == 0) {
-    SLG_PCASE(0, 0, SLG_PLAN_C1) SLG_PCASE(0, 1, SLG_PLAN_C1)
-    SLG_PCASE(0, 0, SLG_PLAN_C1 | kPlanGray) SLG_PCASE(0, 1, SLG_PLAN_C1 | kPlanGray)
-#undef SLG_PCASE
-  }
-#endif
-#define SLG_CASE(RM, X, R) if (row_mode == RM && x64 == X && rays == R) return main3_kernel<RM, X, SRC, R, false>;
-#ifdef SLG_FAST_BUILD   // register/spill inspection builds only: the benchmark's instance alone
-  if (plan == SLG_PLAN_C2 && row_mode == 1 && x64 == 0 && rays == SLG_RAYS_PINHOLE && SRC == 1)
-    return main3_kernel<1, 0, 1, 1, false, SLG_PLAN_C2>;
-  SLG_CASE(1, 0, 1)
-  return nullptr;
-#endif
-  SLG_CASE(0, 0, 0) SLG_CASE(0, 0, 1) SLG_CASE(0, 1, 0) SLG_CASE(0, 1, 1)
-  SLG_CASE(1, 0, 0) SLG_CASE(1, 0, 1) SLG_CASE(1, 1, 0) SLG_CASE(1, 1, 1)
-  SLG_CASE(2, 0, 0) SLG_CASE(2, 0, 1) SLG_CASE(2, 1, 0) SLG_CASE(2, 1, 1)
-#undef SLG_CASE
-  return nullptr;
+  return hit->fn;
 }
 
 // Output + workspace pointers of one view (the per-view half of fill_out).
@@ -3016,9 +2426,9 @@ int fill_view(ViewIO& io, const slg_cloud* out, const slg_tri_params* tp, int64_
 }
 
 // One main3 launch over mp.n_views views (<= kMaxViews), then the row_mode-2 tails.
-int launch_main3(Main3Fn fn, Main3Params& mp, const slg_tri_params* tp, const slg_cloud* outs, hipStream_t s) {
-  if (!fn) return fail(SLG_ERR_UNSUPPORTED, "no kernel for this configuration (SLG_DBG profiling: "
-                                            "row_mode 1, f32, frames, pinhole only)");
+int launch_main3(Main3Fn fn, const char* why, Main3Params& mp, const slg_tri_params* tp, const slg_cloud* outs,
+                 hipStream_t s) {
+  if (!fn) return fail(SLG_ERR_UNSUPPORTED, "%s", why ? why : "no kernel for this configuration");
   mp.c.dbg = debug_flags();
   mp.c.help_after = help_after();
   const int64_t grid = int64_t(mp.n_fin) * mp.fin_blocks + mp.c.n_tiles * mp.n_views;
@@ -3044,7 +2454,6 @@ int check_batch(const slg_capture* caps, int n_views) {
   for (int v = 0; v < n_views; ++v) {
     const int rc = check_capture(&caps[v]);
     if (rc) return rc;
-    if (!caps[v].texture && !SLG_MASK_FIRST) return fail(SLG_ERR_INVALID, "capture %d: texture is NULL", v);
     if (reinterpret_cast<uintptr_t>(caps[v].texture) & 7) return fail(SLG_ERR_INVALID, "texture must be 8-byte aligned");
     if (caps[v].height != caps[0].height || caps[v].width != caps[0].width)
       return fail(SLG_ERR_INVALID, "all views of a batch must share one geometry");
@@ -3057,7 +2466,7 @@ int check_batch(const slg_capture* caps, int n_views) {
 int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* dp, const slg_calib* calib,
                 const slg_tri_params* tp, char* ws, int64_t ws_stride, const slg_cloud* outs,
                 void* const* timing_events, hipStream_t s, const slg_capture* next = nullptr, int n_next = 0,
-                char* fin_ws = nullptr, int n_fin = 0, bool solo = false) {
+                char* fin_ws = nullptr, int n_fin = 0) {
   if (!caps || n_views < 1 || !dp || !ws || !outs) return fail(SLG_ERR_INVALID, "NULL argument");
   int rc = check_batch(caps, n_views);
   if (rc) return rc;
@@ -3108,7 +2517,8 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
     }
     // a mixed launch runs the generic instance (per-view test); a plan instance is all one kind
     if (plan > 0 && any_gray) plan = all_gray ? (plan | kPlanGray) : 0;
-    const Main3Fn fn = pick_main<1>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode, plan < 0 ? 0 : plan, solo);
+    const char* why = nullptr;
+    const Main3Fn fn = pick_main(1, tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode, plan < 0 ? 0 : plan, &why);
     for (int k = 0; k < mp.n_views; ++k) {
       const int v = v0 + k;
       ViewIO& io = mp.v[k];
@@ -3129,11 +2539,6 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
       }
     }
     mp.n_fin = launch == 0 ? n_fin : 0;             // the first launch finishes them all
-    if (solo) {                                     // (one view, Otsu: fused_solo)
-      mp.solo = 1;
-      mp.n_state_words = n_state_words(n_px);
-      mp.pad_zero = mp.c.n_tiles * kTilePx - n_px;
-    }
     if (mp.n_fin) {
       const int64_t nb = (mp.c.n_tiles + 127) / 128;   // ~128 partials (128 KB) per workgroup
       mp.fin_blocks = int(nb < 1 ? 1 : (nb > kPartsBlocksMax ? kPartsBlocksMax : nb));
@@ -3146,7 +2551,7 @@ int fused_batch(const slg_capture* caps, int n_views, const slg_decode_params* d
       }
     }
     if (timing_events && timing_events[2 * launch]) (void)hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * launch]), s);
-    rc = launch_main3(fn, mp, tp, &outs[v0], s);
+    rc = launch_main3(fn, why, mp, tp, &outs[v0], s);
     if (rc) return rc;
     if (timing_events && timing_events[2 * launch + 1]) (void)hipEventRecord(static_cast<hipEvent_t>(timing_events[2 * launch + 1]), s);
   }
@@ -3416,6 +2821,30 @@ extern "C" {
 
 int32_t slg_version(void) { return SLG_ABI_VERSION; }
 
+#ifndef SLG_BUILD_ID
+#define SLG_BUILD_ID "unknown"
+#endif
+const char* slg_build_id(void) { return SLG_BUILD_ID; }
+
+int32_t slg_kernel_table(char* buf, int64_t cap) {
+  if (!buf || cap < 1) return -fail(SLG_ERR_INVALID, "buf NULL or cap < 1");
+  int64_t at = 0;
+  int32_t missing = 0;
+  buf[0] = 0;
+  for (const Main3Inst& k : kMain3Table) {
+    const std::string name = main3_symbol(k);
+    const bool has = device_has(name);
+    missing += has ? 0 : 1;
+    const std::string line = name + (has ? "\t1\n" : "\t0\n");
+    if (at + int64_t(line.size()) < cap) {
+      memcpy(buf + at, line.data(), line.size());
+      at += int64_t(line.size());
+      buf[at] = 0;
+    }
+  }
+  return missing;
+}
+
 const char* slg_last_error(void) { return g_err; }
 
 int64_t slg_workspace_bytes(int64_t n_pixels) { return n_pixels > 0 ? ws_total(n_pixels) : kHeaderBytes; }
@@ -3492,22 +2921,9 @@ int32_t slg_triangulate(const slg_maps* maps, const slg_calib* calib, const slg_
   if (rc) return rc;
   m3.v[0].in_col = maps->col; m3.v[0].in_row = maps->row; m3.v[0].in_mask = maps->mask;
   m3.v[0].texture = maps->texture;
-  return launch_main3(pick_main<0>(tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode), m3, tp, out, s);
-}
-
-#if SLG_SOLO_PROF
-extern "C" int32_t slg_solo_prof_read(void* host, int64_t n_words) {   // (A/B builds only)
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_solo_rec), size_t(n_words) * 8) == hipSuccess ? 0 : 2;
-}
-#endif
-
-// One-view fused launches that count their own Otsu histograms (main3 SOLO: no stats launch
-// before them) with SLG_SOLO=1.  Off by default: 93.5 vs 60.8 us per one-view call, the last
-// chunk's ticket lands ~34 us in (its loads queue behind the other workgroups' frame reads) and
-// the finisher's Otsu takes ~24 us beside them (12.7 alone): tools/solo_prof.py, profiles/r5o.
-static bool solo_enabled() {
-  const char* e = getenv("SLG_SOLO");               // (read per call: tests switch it)
-  return e && e[0] == '1';
+  const char* why = nullptr;
+  const Main3Fn fn = pick_main(0, tp->row_mode, tp->xyz_f64 ? 1 : 0, calib->ray_mode, 0, &why);
+  return launch_main3(fn, why, m3, tp, out, s);
 }
 
 static int reconstruct_impl(const slg_capture* cap, const slg_decode_params* dp, const slg_calib* calib,
@@ -3515,15 +2931,6 @@ static int reconstruct_impl(const slg_capture* cap, const slg_decode_params* dp,
                             bool with_stats) {
   if (!cap || !dp || !workspace) return fail(SLG_ERR_INVALID, "NULL argument");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (with_stats && dp->thresh_mode == SLG_THRESH_OTSU && solo_enabled() && !(debug_flags() & kMainDbgBits)) {
-    int rc = check_batch(cap, 1);
-    if (rc) return rc;
-    if (cap->n_frames < 4)
-      return fail(SLG_ERR_NOT_ENOUGH, "Not enough images (got %d, need at least 4).", cap->n_frames);
-    if (!tp) return fail(SLG_ERR_INVALID, "NULL argument");
-    return fused_batch(cap, 1, dp, calib, tp, static_cast<char*>(workspace), 0, out, nullptr, s, nullptr, 0,
-                       nullptr, 0, true);
-  }
   if (with_stats) {
     int rc = check_batch(cap, 1);
     if (!rc) rc = make_plan(cap, dp, nullptr);

@@ -413,6 +413,4 @@ def reconstruct_view(dev: E.DeviceFrames, cfg: E.DecodeConfig, calib: dict, row_
     dc = dc if dc is not None else _device_calib(calib, dev.height, dev.width)
     out = eng.reconstruct(dev, cfg, dc, row_mode, epipolar_tol, xyz_f64=xyz_f64)
     P, C = out.result()
-    if eng.error_flags() & 4:           # a one-view launch's threshold wait gave up (never seen)
-        raise RuntimeError("one-view launch: thresholds not ready (workspace error bit 2)")
     return P.cpu().numpy(), C.cpu().numpy()

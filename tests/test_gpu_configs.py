@@ -296,25 +296,37 @@ def test_valid_bounds_match_histogram_counts(mods, scan):
         assert g >= int(np.count_nonzero(O.mask_processing(v.frames[0], v.frames[1])))
 
 
-@pytest.mark.parametrize("x64", [False, True])
-def test_one_view_solo_launch_matches_pair(mods, scan, monkeypatch, x64):
-    """SLG_SOLO=1 (opt-in): the one-view fused launch that counts its own Otsu histograms gives
-    the stats + fused pair's clouds bit for bit (counts, XYZ, BGR) on 6 full-size C2 views, the
-    oracle's point counts, and raises no SOLO error flag (bit 2)."""
+
+
+def test_concurrent_stats_thresholds(mods, scan):
+    """The stats tickets run without release / acquire fences (agent-scope atomics only, the
+    hardware assumption documented at stats_kernel): four engines' 16-view stats launches on four
+    streams at once, eight rounds, every view's Otsu thresholds (white, clip(white - black)) equal
+    to the oracle's (server/processing.py:63-72)."""
     E, N = mods
+    import ctypes
     import torch
     cal, views = scan
-    cfg = E.DecodeConfig(1920, 1080, 11, 10, "otsu")
-    dcal = E.DeviceCalib(cal, 1080, 1920)
-    eng = E.Reconstructor(1080, 1920)
-    want = _oracle_all(cal, views[:6], (11, 10))
-    for v, (wp, _) in zip(views[:6], want):
-        d = E.DeviceFrames(list(v.frames), v.texture)
-        monkeypatch.setenv("SLG_SOLO", "0")
-        P0, C0 = (t.clone() for t in eng.reconstruct(d, cfg, dcal, 1, xyz_f64=x64).result())
-        monkeypatch.setenv("SLG_SOLO", "1")
-        for _ in range(2):                               # the launch re-arms its own words
-            P1, C1 = eng.reconstruct(d, cfg, dcal, 1, xyz_f64=x64).result()
-            assert eng.error_flags() & 4 == 0
-            assert len(P1) == len(wp)
-            assert torch.equal(P0, P1) and torch.equal(C0, C1)
+    cfg = E.DecodeConfig(1920, 1080, 11, 11, "otsu")
+    dp = cfg.struct()
+    want = []
+    for v in views:
+        w = v.frames[0]
+        b = v.frames[1].astype(np.float32)
+        want.append((O.otsu_threshold(w), O.otsu_threshold(np.clip(w.astype(np.float32) - b, 0, 255).astype(np.uint8))))
+    dev = [E.DeviceFrames(list(v.frames[:2]) + [None] * 2, "gray", n_frames=4) for v in views]
+    engs = [E.BatchReconstructor(1080, 1920, 16, slots=1) for _ in range(4)]
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    groups = [[(9 * e + k) % len(views) for k in range(16)] for e in range(4)]
+    torch.cuda.synchronize()
+    for rnd in range(8):
+        for eng, g, s in zip(engs, groups, streams):
+            caps = (N.Capture * 16)(*[dev[j].capture() for j in g])
+            N.check(N.lib().slg_decode_stats_batch(caps, 16, ctypes.byref(dp), eng._ws(0), eng.ws_stride,
+                                                   E._stream(s)))
+        torch.cuda.synchronize()
+        for eng, g in zip(engs, groups):
+            for k, j in enumerate(g):
+                hdr = eng.header(0, k).cpu().numpy()
+                thr = np.frombuffer(hdr[3104:3120].tobytes(), np.float64)
+                assert (thr[0], thr[1]) == (float(want[j][0]), float(want[j][1])), (rnd, j)

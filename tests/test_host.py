@@ -65,6 +65,79 @@ def test_capture_limits_rejected_before_any_launch():
     assert res["ok_stack"][0] == N.SLG_ERR_INVALID and "NULL" in res["ok_stack"][1]
 
 
+def test_every_fused_kernel_instance_is_in_the_code_object():
+    """The fused kernel's instance table (``slg_kernel_table``, what pick_main can launch) is
+    complete in the production build, and the library's own reading of its gfx950 code object
+    agrees with llvm-readelf on the unbundled code objects (a missing instance would abort the
+    HIP runtime at launch; the library now refuses it instead)."""
+    code = (
+        "import json\n"
+        f"import {PKG}._native as N\n"
+        "print(json.dumps(N.kernel_table()))\n")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, check=True)
+    import json
+    table = json.loads(out.stdout.strip().splitlines()[-1])
+    assert len(table) == 42, len(table)       # 24 generic + 16 plan + 2 profiling instances
+    assert all(table.values()), [k for k, v in table.items() if not v]
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(os.path.join(llvm, "llvm-readelf")):
+        pytest.skip("no llvm-readelf")
+    import tempfile
+    lib = os.path.join(ROOT, PKG, "libslgpu.so")
+    with tempfile.TemporaryDirectory() as td:
+        import shutil
+        copy = os.path.join(td, "lib.so")           # (the unbundled files land beside the input)
+        shutil.copy(lib, copy)
+        subprocess.run([os.path.join(llvm, "llvm-objdump"), "--offloading", copy], cwd=td, capture_output=True,
+                       check=True)
+        syms = set()
+        for f in os.listdir(td):
+            if "gfx950" in f:
+                r = subprocess.run([os.path.join(llvm, "llvm-readelf"), "--symbols", "-W", os.path.join(td, f)],
+                                   capture_output=True, text=True, check=True)
+                syms.update(line.split()[-1] for line in r.stdout.splitlines() if "main3_kernel" in line)
+    assert set(table) <= syms, sorted(set(table) - syms)[:3]
+
+
+def test_build_id_follows_source_content(tmp_path):
+    """Build provenance: the library embeds the digest of its sources + flags; a content-only
+    source change (mtime kept) makes needs_build() true, and the digest of the sources present
+    is what _native.lib() demands of the product library."""
+    import shutil
+    from structured_light_for_3d_model_replication_amd import build as B
+    from structured_light_for_3d_model_replication_amd import _native as N
+    B.build_native()
+    assert B.built_digest() == B.source_digest()
+    assert not B.needs_build()
+    assert N.lib().slg_build_id().decode() == B.BUILD_ID_PREFIX.decode() + B.source_digest()
+    copies = []
+    for p in B.SRCS:
+        q = tmp_path / os.path.basename(p)
+        shutil.copy2(p, q)
+        copies.append(str(q))
+    st = os.stat(copies[2])
+    data = open(copies[2], "rb").read()
+    with open(copies[2], "wb") as f:                 # same length, one byte changed, mtime restored
+        f.write(data[:-2] + bytes([data[-2] ^ 1]) + data[-1:])
+    os.utime(copies[2], ns=(st.st_atime_ns, st.st_mtime_ns))
+    assert B.source_digest(copies) != B.source_digest()
+    old = B.SRCS
+    try:
+        B.SRCS = copies
+        assert B.needs_build()
+    finally:
+        B.SRCS = old
+    assert not B.needs_build()
+
+
+def test_ab_library_must_be_in_tree(tmp_path):
+    """SLG_LIB (A/B builds) only accepts libraries inside the in-tree A/B build directories."""
+    env = dict(os.environ, SLG_LIB=str(tmp_path / "x.so"))
+    r = subprocess.run([sys.executable, "-c", f"import {PKG}._native"], cwd=ROOT, env=env, capture_output=True,
+                       text=True)
+    assert r.returncode != 0 and "A/B libraries must live in" in r.stderr
+
+
 def test_exports_match_ctypes_table():
     from structured_light_for_3d_model_replication_amd import _native as N
     assert sorted(N.EXPORTS) == header_exports()

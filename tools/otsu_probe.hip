@@ -4,7 +4,7 @@
 // otsu_from_hist, oracle/sl_oracle.py).  Histograms: argv[1] = a file of uint32 [k][256] (e.g.
 // tools/otsu_probe.py writes a C2 view's white and clip(white - black) histograms), else
 // synthetic bimodal ones.
-//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off tools/otsu_probe.hip -o /tmp/otsu_probe [-DSLG_OTSU_LDS=0]
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off tools/otsu_probe.hip -o /tmp/otsu_probe
 __device__ unsigned long long g_otsu_marks[8];
 #define SLG_OTSU_MARK(k) (__builtin_amdgcn_s_waitcnt(0), g_otsu_marks[k] = __builtin_amdgcn_s_memtime())
 #include "../structured_light_for_3d_model_replication_amd/csrc/slgpu.hip"
@@ -104,8 +104,8 @@ int main(int argc, char** argv) {
     hipMemcpy(ticks, dt, 16, hipMemcpyDeviceToHost);
     const double want = otsu_host(&hs[j * 256], n);
     printf("{\"hist\": %d, \"n\": %lld, \"thr\": %.1f, \"host\": %.1f, \"us\": %.2f, \"clocks\": %llu, "
-           "\"clocks_per_bin\": %.1f, \"lds_chains\": %d}\n", j, (long long)n, thr, want, ticks[0] / 100.0,
-           (unsigned long long)ticks[1], ticks[1] / 256.0, SLG_OTSU_LDS);
+           "\"clocks_per_bin\": %.1f}\n", j, (long long)n, thr, want, ticks[0] / 100.0,
+           (unsigned long long)ticks[1], ticks[1] / 256.0);
     if (thr != want) rc = 1;
   }
   return rc;
