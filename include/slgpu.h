@@ -289,10 +289,27 @@ int32_t slg_png_gray8_size(const char *path, int32_t *width, int32_t *height);
 int32_t slg_png_gray8_decode(const char *path, uint8_t *out, int64_t cap, int32_t width,
                              int32_t height);
 
+/* Host: any other PNG (colour, gray + alpha, palette, 1-16 bits, Adam7) decoded to exactly what
+ * OpenCV's PNG decoder returns: cv2.imread(f, 0) into gray[height][width] and / or cv2.imread(f)
+ * into bgr[height][width][3] (either may be NULL; caps in bytes).  OpenCV converts through libpng
+ * (png_set_strip_16, png_set_strip_alpha, png_set_palette_to_rgb, png_set_expand_gray_1_2_4_to_8,
+ * then png_set_bgr / png_set_gray_to_rgb / png_set_rgb_to_gray(png, 1, 0.299, 0.587)); that
+ * arithmetic -- gamma tables of gAMA / sRGB files included -- is restated, pinned byte for byte
+ * to libpng 1.6.37 (tests/test_png_color.py), and the files whose colour handling libpng decides
+ * from data not restated (iCCP profiles, duplicate / invalid / disagreeing gAMA and sRGB) go
+ * through the system libpng itself.  info[7]: {width, height, colour type, bit depth, interlace,
+ * restated (1) or libpng (0), decoded by libpng (1)}.  slg_png_info fills info[0..5] only.
+ * Return 0, else non-zero (unreadable, corrupt or unsupported: cv2.imread would return None).
+ * Thread-safe. */
+int32_t slg_png_info(const char *path, int32_t *info /* [6] */);
+int32_t slg_png_read(const char *path, uint8_t *gray, int64_t gray_cap, uint8_t *bgr, int64_t bgr_cap,
+                     int32_t *info /* [7] */);
+
 /* PNG decode on the device (the same cv2.imread of every used frame, for the batch file path):
  * the host only reads the file and checks its chunks, the GPU inflates and un-filters.
  * slg_png_zstream (host): for an 8-bit, non-interlaced PNG of colour type 0 (gray), 2 (RGB),
- * 4 (gray + alpha) or 6 (RGBA), copies the concatenated IDAT payload (the zlib stream) into
+ * 4 (gray + alpha) or 6 (RGBA) -- a colour one only without gAMA / sRGB / iCCP chunks, whose
+ * gray conversion (libpng's gamma path) is slg_png_read's -- copies the concatenated IDAT payload (the zlib stream) into
  * buf (cap bytes; needs zlen + 8, the file size + 8 always suffices) and fills info[4] =
  * {width, height, channels, zlen}; returns 0, else non-zero (any other file, a CRC error, cap
  * too small: decode it the general way).  Thread-safe.

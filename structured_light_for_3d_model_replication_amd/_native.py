@@ -125,6 +125,8 @@ EXPORTS = {
     "slg_png_gray8_size": (c_i32, [ctypes.c_char_p, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
     "slg_png_gray8_decode": (c_i32, [ctypes.c_char_p, c_vp, c_i64, c_i32, c_i32]),
     "slg_png_zstream": (c_i32, [ctypes.c_char_p, c_vp, c_i64, ctypes.POINTER(c_i32)]),
+    "slg_png_info": (c_i32, [ctypes.c_char_p, ctypes.POINTER(c_i32)]),
+    "slg_png_read": (c_i32, [ctypes.c_char_p, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(c_i32)]),
     "slg_png_raw_bytes": (c_i64, [c_i32, c_i32, c_i32]),
     "slg_png_decode_device": (c_i32, [c_vp, c_i32, c_vp, c_vp]),
     "slg_stream_create_reserving": (c_i32, [c_i32, c_vp]),

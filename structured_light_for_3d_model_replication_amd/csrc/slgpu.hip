@@ -1988,9 +1988,13 @@ __global__ __launch_bounds__(kBlock) void row_tail_kernel(WsHeader* ws, const vo
 // Colour captures (the reference's phone path uploads canvas PNGs, frontend/App.tsx:234-247,
 // saved as-is by server/server.py:86): cv2.imread(f, 0) turns each frame to gray and
 // cv2.imread(files[0]) gives frame 0 as BGR.  One upload of the decoded RGB(A) frames feeds
-// both: gray planes into the frame stack (libpng's rgb_to_gray 15-bit fixed point for PNG,
-// OpenCV's BGR2GRAY 14-bit weights for BMP -- restated, parity unpinned) and frame 0's BGR
-// texture.  16 pixels per lane: channel bytes are read as 16 x C contiguous bytes.
+// both: gray planes into the frame stack and frame 0's BGR texture.  PNG: libpng's
+// png_do_rgb_to_gray for an 8-bit file without gamma tables (OpenCV's png_set_rgb_to_gray(png,
+// 1, 0.299, 0.587)): (9797 r + 19234 g + 3737 b) >> 15, truncated, r where r == g == b --
+// pinned to libpng 1.6.37 (tests/test_png_color.py); gAMA / sRGB / iCCP files never come here
+// (slg_png_zstream refuses them; the host decodes them).  BMP: OpenCV's BGR2GRAY 14-bit weights,
+// restated (parity unpinned: no OpenCV here).  16 pixels per lane: channel bytes are read as
+// 16 x C contiguous bytes.
 constexpr int kRgbPx = 16;
 __global__ __launch_bounds__(kBlock) void rgb_gray_kernel(const uint8_t* rgb, int32_t channels, int64_t n_px,
                                                           int64_t src_stride, uint8_t* gray, int64_t gray_stride,
@@ -2004,10 +2008,10 @@ __global__ __launch_bounds__(kBlock) void rgb_gray_kernel(const uint8_t* rgb, in
   uint32_t g4[kRgbPx / 4] = {0, 0, 0, 0};
 #pragma unroll
   for (int k = 0; k < kRgbPx; ++k) {
-    if (k >= n) break;
+    if (k >= n) continue;
     const uint32_t r = src[k * channels], g = src[k * channels + 1], b = src[k * channels + 2];
     const uint32_t y = bmp ? (b * 1868u + g * 9617u + r * 4899u + 8192u) >> 14
-                           : (r * 9797u + g * 19234u + b * 3737u + 16384u) >> 15;
+                           : (r == g && r == b) ? r : (r * 9797u + g * 19234u + b * 3737u) >> 15;
     g4[k >> 2] |= (y & 0xffu) << (8 * (k & 3));
     if (bgr0 && f == 0) {
       bgr0[(px0 + k) * 3] = uint8_t(b);

@@ -4,11 +4,14 @@
   first, then ``*.png`` (``server/processing.py:49-54``); ``SLSystem.generate_cloud`` globs
   ``*.png`` first, then ``*.bmp`` (``server/sl_system.py:518-520``); both ``sorted``.
 * ``imread_gray`` / ``imread_bgr`` stand in for ``cv2.imread(path, 0)`` / ``cv2.imread(path)``
-  (OpenCV is not in the image).  8-bit grayscale files — what the reference's capture writes
-  and what every test uses — decode identically (identity).  Colour files are converted with
-  libpng's ``rgb_to_gray`` fixed-point weights for PNG and OpenCV's ``BGR2GRAY`` weights for
-  BMP: that arithmetic is restated from the libraries' published formulas and is parity
-  unpinned (no OpenCV here to check against).  Decoding runs on a host thread pool.
+  (OpenCV is not in the image).  PNGs: 8-bit grayscale files -- what the reference's scanner
+  writes -- take the native fast path (identity on the samples); every other PNG (the phone's
+  RGBA canvas captures, ``frontend/App.tsx:234-247``; 16-bit, palette, gray + alpha, Adam7,
+  gAMA / sRGB / iCCP tagged) goes through ``slg_png_read``, which returns what OpenCV's libpng
+  calls return, pinned byte for byte to the system libpng 1.6.37 (``tests/test_png_color.py``).
+  BMP and other formats: PIL, with OpenCV's ``BGR2GRAY`` 14-bit weights for colour BMPs --
+  restated from OpenCV's published C, parity unpinned (no OpenCV here).  Decoding runs on a
+  host thread pool.
 """
 from __future__ import annotations
 
@@ -42,24 +45,28 @@ def _open(path):
 
 
 def _to_gray(im, path) -> np.ndarray:
+    """PIL image of a non-PNG file -> ``cv2.imread(path, 0)`` (8-bit samples)."""
+    if im.mode == "P":
+        im = im.convert("RGBA" if "transparency" in im.info else "RGB")
     a = np.asarray(im)
     if a.dtype == np.uint16:
         a = (a >> 8).astype(np.uint8)
     if a.ndim == 2:
         return np.ascontiguousarray(a, dtype=np.uint8)
+    if a.shape[2] < 3:                                # gray + alpha
+        return np.ascontiguousarray(a[..., 0], dtype=np.uint8)
     rgb = a[..., :3].astype(np.uint32)
     r, g, b = rgb[..., 0], rgb[..., 1], rgb[..., 2]
-    if str(path).lower().endswith(".bmp"):
-        # OpenCV icvCvt_BGR2Gray_8u_C3C1R: (b*1868 + g*9617 + r*4899 + 8192) >> 14
-        y = (b * 1868 + g * 9617 + r * 4899 + 8192) >> 14
-    else:
-        # libpng png_set_rgb_to_gray(…, 0.299, 0.587) 15-bit fixed point, 8-bit path
-        y = (r * 9797 + g * 19234 + b * 3737 + 16384) >> 15
-    return y.astype(np.uint8)
+    # OpenCV icvCvt_BGR2Gray_8u_C3C1R: (b*1868 + g*9617 + r*4899 + 8192) >> 14
+    return ((b * 1868 + g * 9617 + r * 4899 + 8192) >> 14).astype(np.uint8)
+
+
+def _is_png(path) -> bool:
+    return str(path).lower().endswith(".png") and not os.environ.get("SLG_PNG_PIL")
 
 
 def _is_png_gray8(path) -> bool:
-    if not str(path).lower().endswith(".png") or os.environ.get("SLG_PNG_PIL"):
+    if not _is_png(path):
         return False
     import ctypes
     from . import _native as N
@@ -70,7 +77,7 @@ def _is_png_gray8(path) -> bool:
 def _png_gray8(path):
     """Native fast path (``slg_png_gray8_*``): an 8-bit grayscale PNG decoded without PIL;
     ``None`` for any other file (decoded the general way below)."""
-    if not str(path).lower().endswith(".png") or os.environ.get("SLG_PNG_PIL"):
+    if not _is_png(path):
         return None
     import ctypes
     from . import _native as N
@@ -85,11 +92,35 @@ def _png_gray8(path):
     return out
 
 
+def png_read(path, gray: bool = True, bgr: bool = False):
+    """``slg_png_read``: ``(gray [H, W] or None, bgr [H, W, 3] or None)`` as OpenCV's PNG decoder
+    returns them, or None for a file cv2.imread cannot read."""
+    import ctypes
+    from . import _native as N
+    L = N.lib()
+    bp = os.fsencode(path)
+    info = (ctypes.c_int32 * 7)()
+    if L.slg_png_info(bp, info) != 0:
+        return None
+    h, w = info[1], info[0]
+    g = np.empty((h, w), dtype=np.uint8) if gray else None
+    c = np.empty((h, w, 3), dtype=np.uint8) if bgr else None
+    vp = ctypes.c_void_p
+    rc = L.slg_png_read(bp, vp(g.ctypes.data) if gray else None, g.size if gray else 0,
+                        vp(c.ctypes.data) if bgr else None, c.size if bgr else 0, info)
+    return None if rc != 0 else (g, c)
+
+
 def imread_gray(path) -> np.ndarray:
     """``cv2.imread(path, 0)``; raises like ``None.astype`` would for unreadable files."""
     a = _png_gray8(path)
     if a is not None:
         return a
+    if _is_png(path):
+        r = png_read(path, gray=True)
+        if r is None:
+            raise AttributeError("'NoneType' object has no attribute 'astype'")
+        return r[0]
     im = _open(path)
     if im is None:
         raise AttributeError("'NoneType' object has no attribute 'astype'")
@@ -101,14 +132,23 @@ def imread_bgr(path) -> np.ndarray:
     a = _png_gray8(path)
     if a is not None:
         return np.repeat(a[..., None], 3, axis=-1)
+    if _is_png(path):
+        r = png_read(path, gray=False, bgr=True)
+        if r is None:
+            raise AttributeError("'NoneType' object has no attribute 'reshape'")
+        return r[1]
     im = _open(path)
     if im is None:
         raise AttributeError("'NoneType' object has no attribute 'reshape'")
+    if im.mode == "P":
+        im = im.convert("RGBA" if "transparency" in im.info else "RGB")
     a = np.asarray(im)
     if a.dtype == np.uint16:
         a = (a >> 8).astype(np.uint8)
     if a.ndim == 2:
         return np.repeat(a[..., None], 3, axis=-1).astype(np.uint8)
+    if a.shape[2] < 3:
+        return np.repeat(a[..., :1], 3, axis=-1).astype(np.uint8)
     return np.ascontiguousarray(a[..., 2::-1][..., :3], dtype=np.uint8)
 
 

@@ -276,6 +276,8 @@ def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", 
             pool.put(buf)                 # (every decode has stopped writing into it)
             raise
         return HostView(folder, len(files), H, W, stride, "gray", stack, pinned=[buf])
+    if FR._is_png(files[0]):
+        return _read_png_general(folder, files, need, pool)
     # colour (or non-PNG) captures: decoded RGB(A) frames, converted to gray on the device
     first = _decode_rgb(files[0])
     if first.ndim == 2:                               # a gray file the fast path does not take
@@ -310,6 +312,46 @@ def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", 
     weights = N.GRAY_BMP if files[0].lower().endswith(".bmp") else N.GRAY_PNG
     return HostView(folder, len(files), H, W, (n_px + 15) // 16 * 16, "rgb", stack, channels=C,
                     weights=weights, pinned=[buf])
+
+
+def _read_png_general(folder: str, files, need, pool: PinnedPool) -> HostView:
+    """Any PNG capture the gray fast path does not take (colour / RGBA phone captures, 16-bit,
+    palette, Adam7, gAMA / sRGB / iCCP tagged): every used frame decoded on the host threads
+    straight into the pinned gray stack, as cv2.imread(f, 0) returns it, and frame 0's
+    cv2.imread(f) into the pinned texture (``slg_png_read``, pinned to libpng with OpenCV's calls).
+    A gray file's texture is its frame 0 replicated: GRAY texture mode, no texture buffer."""
+    L = N.lib()
+    info0 = (ctypes.c_int32 * 7)()
+    if L.slg_png_info(os.fsencode(files[0]), info0) != 0:
+        raise AttributeError("'NoneType' object has no attribute 'astype'")   # cv2.imread -> None
+    W, H, color = info0[0], info0[1], bool(info0[2] & 2)
+    n_px = H * W
+    stride = (n_px + 15) // 16 * 16
+    buf = pool.get(len(files) * stride)
+    stack = buf.view(len(files), stride)
+    base = stack.data_ptr()
+    tbuf = pool.get(n_px * 3) if color else None
+    order = list(need) if (0 in need or not color) else [0] + list(need)
+
+    def one(i):
+        info = (ctypes.c_int32 * 7)()
+        tex = i == 0 and tbuf is not None
+        rc = L.slg_png_read(os.fsencode(files[i]), ctypes.c_void_p(base + i * stride), n_px,
+                            ctypes.c_void_p(tbuf.data_ptr()) if tex else None, 3 * n_px if tex else 0, info)
+        if rc != 0:
+            if L.slg_png_info(os.fsencode(files[i]), info) == 0 and (info[0], info[1]) != (W, H):
+                raise ValueError("all frames must have the same size")
+            raise AttributeError("'NoneType' object has no attribute 'astype'")
+        if (info[0], info[1]) != (W, H):
+            raise ValueError("all frames must have the same size")
+    try:
+        FR.decode_all(one, order)
+    except BaseException:
+        pool.put(buf)
+        pool.put(tbuf)
+        raise
+    return HostView(folder, len(files), H, W, stride, "gray", stack, texture=tbuf.view(n_px, 3) if color else None,
+                    pinned=[buf] + ([tbuf] if color else []))
 
 
 def _gray_mode(hv: HostView) -> bool:
