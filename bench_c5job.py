@@ -9,15 +9,17 @@ the ranks in contiguous blocks (``distributed.shard_range``: all 576 on one GPU 
 frames + 14 GB of textures + the clouds fit its 288 GB -- or 72 per rank, one object each, on
 8), staged in HBM, and one step is :class:`jobs.ResidentJob` over the rank's block: fused
 launches of ``--batch`` views on the two-stream carried-Otsu pipeline, every cloud written to its
-own region of one packed arena.  The capacity hints come from the job itself: a device sizing
-pass over every view's white / black (jobs.device_capacity_hints -- the Otsu histograms bound each
-view's valid pixels), timed and reported beside the job; no earlier pass over the frames.
+own region of one packed arena.  The job sizes itself inside its own launches: the kernel that
+finishes a view's Otsu thresholds also reserves the view's arena region with one atomicAdd on a
+device cursor (min(#white >= smin, #(white - black) >= cmin) points, an upper bound of its count:
+jobs.ResidentJob's device-reserved arena) -- no sizing pass, no host sync, nothing to add to the
+step time.
 
 Views of one object come from ``--distinct`` rendered captures per object (synth.render_view,
 seed 1000*object + k, staggered turntable angles), each job view an HBM copy of its own: the
 kernel streams every view's 381.5 MB from HBM, as it would distinct captures.  The timed region
-is the whole job, its four priming stats passes included; ``value_with_sizing`` adds the sizing
-pass.  Verification (outside the timing): no view overflows its hint, every view's cloud equals
+is the whole job, its four priming stats passes and every reservation included.  Verification
+(outside the timing): no view is refused by the arena, the reserved regions are disjoint, every view's cloud equals
 its source's single-view cloud bit for bit, and one source's cloud equals the oracle's; a failed
 verification makes ``value`` null and the exit status non-zero.
 """
@@ -98,7 +100,7 @@ def main(args, wl):
     n_views = hi - lo
     F = sources[0].n_frames
     per_view = F * sources[0].stride + 3 * H * W
-    # (a pre-check only: the device hints, an upper bound of the counts, are known once staged)
+    # (a pre-check only: the reservations, an upper bound of the counts, are made by the job)
     need = n_views * per_view + int(1.15 * sum(exact)) * 15 + 4 * args.batch * 4 * (1 << 26)
     free, total = torch.cuda.mem_get_info(dev)
     log(f"[rank {rank}] staging {n_views} views: {n_views * per_view / 1e9:.1f} GB of frames + textures, "
@@ -113,19 +115,11 @@ def main(args, wl):
         torch.cuda.synchronize()
         log(f"[rank {rank}] staged {len(views)}/{n_views} views ({time.perf_counter() - t:.1f}s)")
     B = max(1, min(args.batch, E.MAX_VIEWS_PER_LAUNCH))
-    # the job sizes its arena on the device: one stats pass over white / black per view
-    sizer = E.BatchReconstructor(H, W, 8, device=dev, slots=1)    # 8 workspaces (~1.8 GB at 4K)
-    J.device_capacity_hints(views[:1], cfg, sizer)                  # (warm: code objects, clocks)
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    hints = J.device_capacity_hints(views, cfg, sizer)             # ends with a host sync
-    sizing_s = time.perf_counter() - t
-    del sizer
-    torch.cuda.empty_cache()                                        # its workspaces, for the arena
+    # the job reserves each view's arena region itself, inside its launches (device cursor)
     job = J.ResidentJob(views, cfg, dcal, batch=B, row_mode=row_mode, epipolar_tol=tol, xyz_f64=False,
-                        capacity_hints=hints, device=dev)
-    log(f"[rank {rank}] device sizing {sizing_s * 1e3:.2f} ms: arena {job.arena_points * 15 / 1e9:.2f} GB "
-        f"(exact counts would take {(sum(exact) + H * W) * 15 / 1e9:.2f} GB)")
+                        device=dev)
+    log(f"[rank {rank}] device-reserved arena of {job.arena_points * 15 / 1e9:.2f} GB "
+        f"(exact counts take {sum(exact) * 15 / 1e9:.2f} GB)")
     s0, s1 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
     K, Wm = args.steps, args.warmup
     for _ in range(max(1, Wm)):
@@ -148,13 +142,17 @@ def main(args, wl):
     kern_ms = ev[0].elapsed_time(ev[1])
 
     counts = job.host_counts()
+    offs = job.host_offsets()
+    reserved = int(job.cursor.item())                     # points the last job reserved
     verify = None
     if not args.no_verify:
         over = job.overflowed(counts)
+        spans = sorted((o, o + n) for o, n in zip(offs, counts) if o >= 0)
+        disjoint = all(a[1] <= b[0] for a, b in zip(spans, spans[1:])) and (not spans or spans[-1][1] <= job.arena_points)
         same = all(torch.equal(job.cloud(j, counts)[0], first[plan[j]][0]) and
                    torch.equal(job.cloud(j, counts)[1], first[plan[j]][1]) for j in range(n_views))
-        verify = {"views": n_views, "counts_equal_single_view_path": counts == exact, "overflowed": over,
-                  "damaged": job.damaged(counts),
+        verify = {"views": n_views, "counts_equal_single_view_path": counts == exact, "refused": over,
+                  "regions_disjoint": bool(disjoint), "damaged": job.damaged(counts),
                   "clouds_equal_single_view_path_bitwise": bool(same)}
         if rank == 0:
             from oracle import sl_oracle as O
@@ -170,7 +168,8 @@ def main(args, wl):
                           oracle_colours_equal=bool(len(Po) == len(gx) and np.array_equal(first[0][1].cpu().numpy(), Co)),
                           oracle_xyz_max_rel=rel)
             verify["oracle_ok"] = bool(verify["oracle_colours_equal"] and rel is not None and rel <= 1e-4)
-        ok = verify["counts_equal_single_view_path"] and not over and same and verify.get("oracle_ok", True)
+        ok = (verify["counts_equal_single_view_path"] and not over and disjoint and same
+              and verify.get("oracle_ok", True))
         verify["ok"] = bool(ok)
         if not ok:
             log(f"[rank {rank}] VERIFY FAILED: {verify}")
@@ -190,10 +189,6 @@ def main(args, wl):
         dist.all_reduce(tk, op=dist.ReduceOp.MAX)
     all_pts, dense, mf, all_views = (float(x) for x in stats.tolist())
     dt_max, kern_max = (float(x) for x in tk.tolist())
-    sz = torch.tensor([sizing_s], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(sz, op=dist.ReduceOp.MAX)
-    sizing_max = float(sz.item())
     if rank == 0:
         job_s = kern_max / 1e3 / K                     # HIP events on s0 around the K jobs / K
         achieved = dense / job_s / 1e9 / world         # per GPU: each rank streams its own block
@@ -202,7 +197,6 @@ def main(args, wl):
         out = {
             "metric": bench.METRIC,
             "value": value if all_ok else None,
-            "value_with_sizing": (round(all_pts / (dt_max / K + sizing_max) / 1e6, 2) if all_ok else None),
             "unit": "Mpoints/s",
             "n_gpus": world,
             "steps": K,
@@ -222,15 +216,15 @@ def main(args, wl):
                        "points_per_job": int(all_pts), "points_per_view": int(all_pts / max(1.0, all_views)),
                        "us_per_view": round(dt_max / K / max(1.0, all_views / world) * 1e6, 3),
                        "job_ms_events": round(job_s * 1e3, 4), "batch_views": B,
-                       "capacity_hints": {
-                           "source": "device sizing pass (jobs.device_capacity_hints): one batched stats pass over "
-                                     "every view's white + black, min(#white >= smin, #(white-black) >= cmin) from "
-                                     "the Otsu histograms -- an upper bound of each view's row_mode 0/1 points; "
-                                     "no earlier pass over the job",
-                           "sizing_ms_rank0": round(sizing_s * 1e3, 3), "sizing_ms_max": round(sizing_max * 1e3, 3),
+                       "capacity": {
+                           "source": "device-reserved arena (jobs.ResidentJob, slg_workspace_set_arena): the kernel "
+                                     "that finishes a view's Otsu thresholds reserves min(#white >= smin, "
+                                     "#(white-black) >= cmin) points with one atomicAdd -- inside the timed job, "
+                                     "no sizing pass",
                            "arena_gb_rank0": round(job.arena_points * 15 / 1e9, 2),
-                           "exact_counts_gb_rank0": round((sum(exact) + H * W) * 15 / 1e9, 2),
-                           "hint_over_count": round(sum(hints) / max(1, sum(exact)), 4)},
+                           "reserved_gb_rank0": round(reserved * 15 / 1e9, 2),
+                           "exact_counts_gb_rank0": round(sum(exact) * 15 / 1e9, 2),
+                           "reserved_over_count": round(reserved / max(1, sum(exact)), 4)},
                        "hbm_resident_gb_rank0": round(n_views * per_view / 1e9, 1),
                        "parallelism": f"view-sharded x{world} (contiguous blocks of the job), no collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": bench.HBM_PEAK_GBS, "unit": "GB/s",

@@ -162,6 +162,19 @@ int64_t slg_workspace_bytes(int64_t n_pixels);
 /* Zero a freshly allocated workspace (once; the kernels keep it consistent afterwards). */
 int32_t slg_workspace_init(void *workspace, int64_t workspace_bytes, void *stream);
 
+/* Resident jobs (jobs.ResidentJob): bind n_slices workspace slices (ws_stride apart) to one
+ * packed output arena of capacity_points points.  From then on, whichever kernel sets a slice's
+ * thresholds (stats, partials, a fused launch's finishing workgroups) also reserves the view's
+ * region: atomicAdd(*cursor, need) with need = min(#white >= smin, #(white - black) >= cmin) x
+ * points_per_valid (1: row_mode 0/1, 2: row_mode 2) -- an upper bound of the view's points -- so
+ * no view can write past its region; no room left: the view stores nothing.  The fused launches
+ * then take every bound slice's cloud (slg_cloud) as: xyz / bgr = the arena's base, capacity =
+ * the arena's, count -> int64[2] = {points, first point index in the arena or -1 (no room: re-run
+ * the view)}.  The caller zeroes *cursor (device int64) before each job; cursor NULL unbinds.
+ * Asynchronous on `stream`. */
+int32_t slg_workspace_set_arena(void *workspace, int64_t ws_stride, int32_t n_slices, int64_t *cursor,
+                                int64_t capacity_points, int32_t points_per_valid, void *stream);
+
 /* Histograms + thresholds of the valid mask into the workspace; also arms the workspace for
  * the next slg_decode / slg_reconstruct on the same stream. */
 int32_t slg_decode_stats(const slg_capture *cap, const slg_decode_params *dp, void *workspace,

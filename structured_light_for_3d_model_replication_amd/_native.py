@@ -89,6 +89,7 @@ EXPORTS = {
     "slg_last_error": (ctypes.c_char_p, []),
     "slg_workspace_bytes": (c_i64, [c_i64]),
     "slg_workspace_init": (c_i32, [c_vp, c_i64, c_vp]),
+    "slg_workspace_set_arena": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp]),
     "slg_decode_stats": (c_i32, [ctypes.POINTER(Capture), ctypes.POINTER(DecodeParams), c_vp, c_vp]),
     "slg_decode": (c_i32, [ctypes.POINTER(Capture), ctypes.POINTER(DecodeParams), c_vp,
                            c_vp, c_vp, c_vp, c_vp]),

@@ -81,14 +81,23 @@ struct WsHeader {
   // which the clipped histogram cannot count); their minimum bounds the valid pixels, so the
   // point count of row_mode 0/1 (resident jobs size their clouds with it).  n_px otherwise.
   int64_t above[2];
-  uint32_t reserved[4];
-  uint64_t pad3[4];
+  // Resident-job arena (slg_workspace_set_arena; NULL cursor: none).  The Otsu tail that sets a
+  // view's thresholds also reserves its cloud's region: arena_off = atomicAdd(cursor, need),
+  // need = min(above) * arena_mult (an upper bound of its points), or -1 when the arena has no
+  // room left (the fused launch then stores nothing for it; the host re-runs it).
+  int64_t arena_off;
+  int32_t arena_mult;      // points per valid pixel at most: 1 (row_mode 0/1) or 2 (row_mode 2)
+  int32_t pad4;
+  unsigned long long* arena_cursor;
+  int64_t arena_cap;       // points the arena holds
+  uint64_t pad3[2];
 };
 constexpr int kHistCopies = 16;            // partial histograms: blocks spread their atomics
 constexpr int64_t kHistPartOff = 8192;      // uint32 [kHistCopies][2][256] after the header
 constexpr int64_t kHeaderBytes = 65536;
 static_assert(sizeof(WsHeader) <= kHistPartOff, "header");
-static_assert(offsetof(WsHeader, error) == 3084 && offsetof(WsHeader, above) == 3136,
+static_assert(offsetof(WsHeader, error) == 3084 && offsetof(WsHeader, above) == 3136 &&
+              offsetof(WsHeader, arena_off) == 3152,
               "header offsets the host reads (engine.py: error word, WS_ABOVE_OFF)");
 
 __host__ __device__ inline int64_t n_tiles_of(int64_t n_px) { return (n_px + kTilePx - 1) / kTilePx; }
@@ -257,6 +266,16 @@ __device__ __attribute__((always_inline)) inline int64_t hist_at_least_wave(cons
     if (b >= m) a += h[b];
   }
   return int64_t(wave_sum(a));
+}
+
+// The resident-job arena reservation of one view, by the thread that finishes its thresholds,
+// from its two `above` counts: see WsHeader::arena_off.
+__device__ inline void arena_reserve(WsHeader* ws, int64_t a0, int64_t a1) {
+  unsigned long long* cur = ws->arena_cursor;
+  if (!cur) return;
+  const int64_t need = (a0 < a1 ? a0 : a1) * int64_t(ws->arena_mult);
+  const int64_t off = int64_t(atomicAdd(cur, (unsigned long long)need));
+  ws->arena_off = off + need <= ws->arena_cap ? off : -1;
 }
 
 // The two serial chains of otsu_wave (q1, then mu1) run on wave-uniform registers fed from LDS:
@@ -591,6 +610,7 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
   __shared__ uint4 s_stage[(kBlock / 64) * 256];   // Otsu: per wave hi/lo nibble planes of w, d
   __shared__ uint32_t s_maxd;
   __shared__ uint32_t s_last;
+  __shared__ int64_t s_above[2];
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int view = blockIdx.y;               // batched launches: one grid row per view
@@ -612,6 +632,7 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
       if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
       ws->above[tid] = p.n_px;                 // manual thresholds: no histogram, no bound
     }
+    if (blockIdx.x == 0 && tid == 0) arena_reserve(ws, p.n_px, p.n_px);
     return;
   }
 
@@ -723,6 +744,7 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
       if ((tid & 63) == 0) {
         if (wave == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
         ws->above[wave] = above;
+        s_above[wave] = above;
       }
     }
   } else if (tid < 2) {
@@ -737,7 +759,10 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
     const int m = int_threshold(thr, tid == 0 ? 0 : -255);
     if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
     ws->above[tid] = p.n_px;                   // (the percentile histogram is black's: no bound)
+    s_above[tid] = p.n_px;
   }
+  __syncthreads();
+  if (tid == 0) arena_reserve(ws, s_above[0], s_above[1]);
   for (int i = tid; i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
   if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
 }
@@ -749,6 +774,7 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
 // workgroup's tile range in flight at once (kPartsInFlight loads per lane), then <= 512 global
 // adds, a ticket, and the same Otsu tail as stats_kernel in the last arriver.
 constexpr int kPartsInFlight = 16;
+constexpr int kPartsLdsWords = 512 + 4 * kOtsuLds + 4;
 constexpr int kPartsBlocksMax = 64;         // workgroups per view (each sums a contiguous tile range)
 
 // One workgroup's share of "thresholds from partials" for one view: workgroup `block` of
@@ -756,12 +782,13 @@ constexpr int kPartsBlocksMax = 64;         // workgroups per view (each sums a 
 // the view's histogram copies, takes a ticket; the last arriver runs Otsu, writes the mask
 // thresholds and resets the histogram state.  Also zeroes the view's look-back words (arming
 // the main launch that will use these thresholds; ordered by the kernel boundary).  256 lanes;
-// hg: 512 words of LDS + 2 x kOtsuLds doubles (16-byte aligned), s_last: one.  Used by
-// parts_kernel and by main3's finishing workgroups.
+// hg: kPartsLdsWords words of LDS (512 histogram words + 2 x kOtsuLds doubles + 2 int64,
+// 16-byte aligned), s_last: one.  Used by parts_kernel and by main3's finishing workgroups.
 __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint32_t* pp, WsHeader* ws, int64_t n_parts, int64_t n_px,
                                 int64_t n_state_words, int64_t pad_zero, int block, int n_blocks,
                                 uint32_t* hg, uint32_t* s_last) {
   const int tid = threadIdx.x, wave = tid >> 6;
+  int64_t* s_above = reinterpret_cast<int64_t*>(hg + 512 + 4 * kOtsuLds);
   const bool act = tid < kBlock;               // the work is laid out for 256 lanes (a 512-lane
   uint32_t* hist_part = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + kHistPartOff);
   uint64_t* states = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + states_off(n_px));
@@ -811,14 +838,17 @@ __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint
     if ((tid & 63) == 0) {
       if (wave == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
       ws->above[wave] = above;
+      s_above[wave] = above;
     }
   }
+  __syncthreads();
+  if (tid == 0) arena_reserve(ws, s_above[0], s_above[1]);
   for (int i = tid; act && i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
   if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
 }
 
 __global__ __launch_bounds__(kBlock) void parts_kernel(StatsParams p) {
-  __shared__ __attribute__((aligned(16))) uint32_t hg[512 + 4 * kOtsuLds];   // + the Otsu tail's LDS
+  __shared__ __attribute__((aligned(16))) uint32_t hg[kPartsLdsWords];   // + the Otsu tail's LDS
   __shared__ uint32_t s_last;
   otsu_from_parts(p.parts[blockIdx.y], p.wsv[blockIdx.y], p.n_parts, p.n_px, p.n_state_words, p.pad_zero,
                   int(blockIdx.x), int(gridDim.x), hg, &s_last);
@@ -1679,7 +1709,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
     const int fv = int(blockIdx.x) / P.fin_blocks;
     otsu_from_parts(P.fin[fv].parts, P.fin[fv].ws, tiles, P.c.n_px, P.n_state_words, P.pad_zero,
                     int(blockIdx.x) - fv * P.fin_blocks, P.fin_blocks, reinterpret_cast<uint32_t*>(s_item), s_bgr);
-    static_assert(512 * 4 + 2 * kOtsuLds * 8 <= sizeof(s_item), "the finishing workgroups' Otsu LDS");
+    static_assert(kPartsLdsWords * 4 <= sizeof(s_item), "the finishing workgroups' Otsu LDS");
     return;
   }
   const int bid = int(blockIdx.x) - n_fin_wg;
@@ -1688,6 +1718,9 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   const int tile = bid / P.n_views;
   const int view = bid - tile * P.n_views;
   const MainParams p = view_params(P, view);
+  // resident-job arena (WsHeader::arena_off, set with the thresholds by an earlier kernel): the
+  // view's column cloud starts at aoff in the arena the cloud pointers name; -1: no room, store nothing
+  const int64_t aoff = p.ws->arena_cursor ? p.ws->arena_off : 0;
   const int64_t tile_px = int64_t(tile) * kTilePx;
   const int64_t px0 = tile_px + int64_t(tid) * kPx;
   const bool tail = tile == tiles - 1;               // block-uniform: guarded reads only here
@@ -1904,6 +1937,7 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
         if (tail) {
           p.ws->totals[s] = int64_t(excl) + agg;
           if (ROW_MODE != 2) *p.count = int64_t(excl) + agg;
+          if (s == 0 && p.ws->arena_cursor) p.count[1] = aoff;   // arena mode: count[2]
         }
       }
     }
@@ -1935,9 +1969,10 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   // as 16 + 8-byte stores -- DESIGN.md §4)
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const int64_t base = int64_t(s_excl[s]);
+    const int64_t base = int64_t(s_excl[s]) + (s == 0 ? aoff : 0);
     XT* gx = reinterpret_cast<XT*>(s == 0 ? p.xyz : p.scratch_xyz);
     uint8_t* gb = s == 0 ? p.bgr : p.scratch_bgr;
+    if (s == 0 && aoff < 0) continue;                // arena without room for the view
 #pragma unroll
     for (int i = 0; i < kIt; ++i) {
       if ((km[s][i] >> lane) & 1ull) {
@@ -1973,15 +2008,17 @@ __global__ __launch_bounds__(kBlock) void row_tail_kernel(WsHeader* ws, const vo
                                                           void* xyz, uint8_t* bgr, int64_t* count) {
   using XT = typename std::conditional<XYZ64 != 0, double, float>::type;
   const int64_t nc = ws->totals[0], nr = ws->totals[1];
+  const int64_t aoff = ws->arena_cursor ? ws->arena_off : 0;     // resident-job arena (main3)
   const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
   if (i == 0) *count = nc + nr;
-  if (i >= nr) return;
+  if (i >= nr || aoff < 0) return;
   const XT* s = reinterpret_cast<const XT*>(sx);
   XT* d = reinterpret_cast<XT*>(xyz);
+  const int64_t q = aoff + nc + i;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    d[(nc + i) * 3 + c] = s[i * 3 + c];
-    bgr[(nc + i) * 3 + c] = sb[i * 3 + c];
+    d[q * 3 + c] = s[i * 3 + c];
+    bgr[q * 3 + c] = sb[i * 3 + c];
   }
 }
 
@@ -2024,6 +2061,18 @@ __global__ __launch_bounds__(kBlock) void rgb_gray_kernel(const uint8_t* rgb, in
   } else {
     for (int k = 0; k < n; ++k) dst[k] = uint8_t(g4[k >> 2] >> (8 * (k & 3)));
   }
+}
+
+// slg_workspace_set_arena: the arena words of n slices' headers.
+__global__ __launch_bounds__(64) void set_arena_kernel(char* ws, int64_t stride, int n, unsigned long long* cursor,
+                                                       int64_t cap, int mult) {
+  const int v = int(blockIdx.x) * 64 + int(threadIdx.x);
+  if (v >= n) return;
+  WsHeader* h = reinterpret_cast<WsHeader*>(ws + int64_t(v) * stride);
+  h->arena_cursor = cursor;
+  h->arena_cap = cap;
+  h->arena_mult = mult;
+  h->arena_off = 0;
 }
 
 // Gray frame stack whose texture is frame 0 replicated (cv2.imread(f) of an 8-bit gray PNG):
@@ -3123,6 +3172,20 @@ int32_t slg_rgb_to_gray(const uint8_t* rgb, int32_t channels, int64_t n_pixels, 
                      dim3(kBlock), 0, static_cast<hipStream_t>(stream), rgb, channels, n_pixels, src_stride, gray,
                      gray_stride, bgr0, weights == SLG_GRAY_BMP ? 1 : 0);
   return check_launch("rgb_gray_kernel");
+}
+
+int32_t slg_workspace_set_arena(void* workspace, int64_t ws_stride, int32_t n_slices, int64_t* cursor,
+                                int64_t capacity_points, int32_t points_per_valid, void* stream) {
+  if (!workspace || n_slices < 1 || (n_slices > 1 && (ws_stride < kHeaderBytes || (ws_stride & 255))))
+    return fail(SLG_ERR_INVALID, "bad workspace / stride");
+  if (cursor && (capacity_points < 0 || (points_per_valid != 1 && points_per_valid != 2)))
+    return fail(SLG_ERR_INVALID, "arena capacity < 0 or points_per_valid not 1 / 2");
+  if (reinterpret_cast<uintptr_t>(cursor) & 7) return fail(SLG_ERR_INVALID, "cursor must be 8-byte aligned");
+  hipLaunchKernelGGL(set_arena_kernel, dim3(unsigned((n_slices + 63) / 64)), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     static_cast<char*>(workspace), ws_stride, int(n_slices),
+                     reinterpret_cast<unsigned long long*>(cursor), cursor ? capacity_points : 0,
+                     cursor ? points_per_valid : 0);
+  return check_launch("set_arena_kernel");
 }
 
 int32_t slg_gray_texture(const uint8_t* frame0, int64_t n_pixels, uint8_t* bgr, void* stream) {

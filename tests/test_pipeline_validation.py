@@ -143,6 +143,7 @@ def test_resident_job_damage_reaches_every_overwritten_view():
     region begins before its last point: those are damaged too (jobs.ResidentJob.damaged)."""
     from structured_light_for_3d_model_replication_amd import jobs as J
     job = J.ResidentJob.__new__(J.ResidentJob)
+    job.device_arena = False                               # a host-packed job (caller hints)
     job.hints = [10, 5, 5, 20, 8]
     job.offsets = [0, 10, 15, 20, 40, 48]
     assert job.damaged([10, 5, 5, 20, 8]) == [] and job.overflowed([10, 5, 5, 20, 8]) == []
