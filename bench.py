@@ -170,21 +170,9 @@ def _cpu_model():
 
 
 def cpu_quota():
-    """CPUs of CPU time this process may use: the cgroup CFS quota (cgroup v2 ``cpu.max``, or v1
-    ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``), rounded up; None when unlimited.  On the GPU
-    box the affinity mask lists every host CPU (256) while the lease's quota is 16."""
-    import math
-    try:
-        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        return None if q == "max" else max(1, math.ceil(int(q) / int(per)))
-    except (OSError, ValueError):
-        pass
-    try:
-        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
-        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
-        return None if q <= 0 else max(1, math.ceil(q / per))
-    except (OSError, ValueError):
-        return None
+    """The cgroup CPU quota (frames.cpu_quota; None when unlimited)."""
+    from structured_light_for_3d_model_replication_amd.frames import cpu_quota as q
+    return q()
 
 
 def _pool_rate(workers, seconds):

@@ -152,9 +152,28 @@ def imread_bgr(path) -> np.ndarray:
     return np.ascontiguousarray(a[..., 2::-1][..., :3], dtype=np.uint8)
 
 
+def cpu_quota():
+    """CPUs of CPU time this process may use: the cgroup CFS quota (cgroup v2 ``cpu.max``, or v1
+    ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``), rounded up; None when unlimited.  On the GPU
+    box the affinity mask lists every host CPU (256) while the lease's quota is 16."""
+    import math
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, math.ceil(q / per))
+    except (OSError, ValueError):
+        return None
+
+
 def decode_threads() -> int:
-    """Host decode threads: ``SLG_DECODE_THREADS``, else the CPUs this process may use, at
-    most 16 (a GPU box's CPU share; more only contends with the PLY writer)."""
+    """Host decode threads: ``SLG_DECODE_THREADS``, else the CPUs this process may use -- the
+    smaller of its affinity mask and its cgroup CPU quota (at most 64: past that the PLY writers
+    and the device group's stream reads want CPUs too)."""
     env = os.environ.get("SLG_DECODE_THREADS")
     if env:
         return max(1, int(env))
@@ -162,7 +181,10 @@ def decode_threads() -> int:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 8
-    return max(1, min(16, n))
+    q = cpu_quota()
+    if q is not None:
+        n = min(n, q)
+    return max(1, min(64, n))
 
 
 _POOLS: dict = {}

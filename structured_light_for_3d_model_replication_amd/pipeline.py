@@ -8,8 +8,9 @@ write an ASCII PLY.  Here the same work is a pipeline whose stages overlap:
   decode needs straight into a **pinned** host frame stack (native 8-bit gray PNG decoder into the
   stack rows; colour frames into a pinned RGB(A) stack, converted on the device);
 * **device decode** (decode stream, issued first): the last folders of a batch of PNG captures
-  (:func:`device_share`) are read as zlib streams only and inflated by ONE GPU launch while the
-  host threads decode the others -- the two decoders' rates add;
+  (:func:`plan_split`, a rate model: the host threads' measured decode rate against one device
+  launch's latency) are read as zlib streams only and inflated by ONE GPU launch while the host
+  threads decode the others -- the two decoders' rates add;
 * **upload** (copy stream): async H2D of a group of up to ``group`` views;
 * **reconstruct** (compute stream): device texture (frame 0 replicated, or frame 0's BGR from the
   colour upload), then ONE batched stats launch + ONE fused decode/triangulate launch for the
@@ -34,7 +35,7 @@ import os
 import threading
 import time
 from collections import deque
-from concurrent.futures import ThreadPoolExecutor, wait
+from concurrent.futures import Future, ThreadPoolExecutor, wait
 from dataclasses import dataclass, field
 
 
@@ -113,15 +114,90 @@ def device_png_enabled() -> bool:
     return device_png_mode() == "all"
 
 
-# Host PNG decode on the box's 16 CPUs: ~70 C2 views/s with two folders in flight (profiles/r5o,
-# 14 ms per view); one device inflate launch: ~220 ms for up to 16 views on a CU mask from
-# png_reserve_every (one wave per stream, a serial Huffman chain each; the launch takes its
-# slowest stream's time).  The device pays only when the host has about that long of its own
-# work: the last n - 22 folders (at most 16) go to ONE device launch started at the beginning,
-# the host threads decode the rest meanwhile.  36 folders, 14 device views: 0.0133-0.0143 s/view,
-# against 0.0136-0.0174 with 10 and 0.0157-0.0177 host-only (profiles/r6g, r6h).
-HOST_AHEAD = 22
+# ---- the host / device split of the PNG decode: a rate model
+# The device inflate is one wave per zlib stream, a serial Huffman chain each, so ONE launch
+# takes about its largest stream's time whatever the number of views (~233 ms for
+# 1080p gray frames at 10-16 views, tools/png_views_bench.py: 0.99 correlation with the largest
+# stream), plus the device group's zlib-stream reads before the launch starts (65-140 ms).  The
+# host decodes at (threads / thread-seconds per frame).  The device takes the LAST n_dev folders
+# so that the host's own share still lasts at least the device's latency: then the batch ends
+# with the host, sooner than host-only; when even the whole batch decodes on the host within
+# that latency, n_dev = 0.  The host's rate is measured (RateMeter: every host frame decode is
+# timed; the first batch of a process measures its first folder before deciding), the device's
+# is updated from every device group's launch, the priors below only seed them.
+HOST_S_PER_MB_PRIOR = 2.5e-3    # thread-seconds per MB of raw samples, 8-bit gray PNG on the host
+                                # (EPYC 9575F, 16 threads: ~70 C2 views/s, 44 x 2.07 MB each, r6g-r6l)
+DEV_S_PER_MB_PRIOR = 0.112      # one inflate launch per MB of its largest frame (233 ms / 2.07 MB, r6e)
+DEV_FIXED_S = 0.07              # the device group's zlib-stream reads before its launch (r6l: 65-140 ms)
 DEVICE_MAX_VIEWS = 16
+
+
+class RateMeter:
+    """Measured decode rates of this process (thread-safe): host thread-seconds per MB of raw
+    samples (each host frame decode timed on its pool thread) and device inflate seconds per MB of
+    a launch's largest frame."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self.host_s = self.host_mb = 0.0
+        self.dev_s = self.dev_mb = 0.0
+
+    def add_host(self, seconds: float, mb: float):
+        with self._lock:
+            self.host_s += seconds
+            self.host_mb += mb
+
+    def add_device(self, seconds: float, mb: float):
+        with self._lock:
+            self.dev_s += seconds
+            self.dev_mb += mb
+
+    def host_measured(self) -> bool:
+        return self.host_mb >= 8.0                  # a few frames' worth
+
+    def host_s_per_mb(self) -> float:
+        return self.host_s / self.host_mb if self.host_measured() else HOST_S_PER_MB_PRIOR
+
+    def dev_s_per_mb(self) -> float:
+        return self.dev_s / self.dev_mb if self.dev_mb > 0 else DEV_S_PER_MB_PRIOR
+
+
+RATES = RateMeter()
+
+
+@dataclass
+class SplitPlan:
+    """What :func:`plan_split` decided and why (logged in the pipeline stats)."""
+    n_dev: int
+    host_s_per_folder: float
+    device_s: float
+    cap: int
+    threads: int
+
+
+def device_view_cap(frames_per_folder: int, n_cus: int) -> int:
+    """Most views one device launch takes at a CU-mask stride measured to keep it at one launch
+    latency (:func:`png_reserve_every` != 0): 15 C2 views of 44 streams at stride 8 on 256 CUs
+    (at 16 views the streams no longer fit any measured-good stride)."""
+    n = DEVICE_MAX_VIEWS
+    while n > 0 and png_reserve_every(n * max(1, frames_per_folder), n_cus) == 0:
+        n -= 1
+    return n
+
+
+def plan_split(n_folders: int, frames_per_folder: int, frame_mb: float, threads: int, host_s_per_mb: float,
+               dev_s_per_mb: float, n_cus: int, dev_fixed_s: float = DEV_FIXED_S) -> SplitPlan:
+    """Device share of a batch: the largest n_dev <= the launch cap whose remaining host share
+    takes at least the device's latency (0 when the host finishes the whole batch sooner)."""
+    threads = max(1, int(threads))
+    per_folder = frames_per_folder * frame_mb * host_s_per_mb / threads
+    device_s = dev_fixed_s + frame_mb * dev_s_per_mb
+    cap = device_view_cap(frames_per_folder, n_cus)
+    n_dev = 0
+    if per_folder > 0:
+        import math
+        n_dev = n_folders - math.ceil(device_s / per_folder)
+    return SplitPlan(max(0, min(cap, n_dev)), per_folder, device_s, cap, threads)
 
 
 _DECODE_STREAMS: dict = {}
@@ -171,15 +247,40 @@ def png_decode_stream(device: int | None = None, n_streams: int | None = None):
     return s
 
 
-def device_share(n_folders: int, mode: str | None = None) -> int:
-    """Folders (the last ones of the batch) whose PNG frames the GPU decodes."""
+def _layout(folder: str, cfg: E.DecodeConfig, order=("bmp", "png")):
+    """(frames the decode reads, MB of raw samples per frame, the device decoder takes them) of a
+    capture folder, from its file list and first PNG header (no decode)."""
+    from .processing import _needed_frames
+    files = FR.discover(folder, order)
+    if len(files) < 4 or not FR._is_png(files[0]):
+        return 0, 0.0, False
+    info = (ctypes.c_int32 * 7)()
+    if N.lib().slg_png_info(os.fsencode(files[0]), info) != 0:
+        return 0, 0.0, False
+    ch = {0: 1, 2: 3, 4: 2, 6: 4}.get(info[2], 0)
+    need = _needed_frames(len(files), cfg) if cfg.variant == "processing" else list(range(len(files)))
+    device_ok = ch > 0 and info[3] == 8 and info[4] == 0 and info[0] * ch <= 24576
+    return len(need), info[0] * info[1] * max(ch, 1) / 1e6, device_ok
+
+
+def device_share(n_folders: int, mode: str | None = None, layout=None, threads: int | None = None) -> int:
+    """Folders (the last ones of the batch) whose PNG frames the GPU decodes: all / none when
+    forced (SLG_PNG_DEVICE=1 / 0), else :func:`plan_split` on ``layout`` = (frames per folder, MB
+    per frame, device-decodable) with the measured rates (SLG_PNG_HOST_AHEAD=k: the last n - k
+    folders, for A/B runs)."""
     mode = device_png_mode() if mode is None else mode
     if mode == "off":
         return 0
     if mode == "all":
         return n_folders
-    ahead = int(os.environ.get("SLG_PNG_HOST_AHEAD", HOST_AHEAD))
-    return max(0, min(DEVICE_MAX_VIEWS, n_folders - ahead))
+    env = os.environ.get("SLG_PNG_HOST_AHEAD")
+    if env is not None:
+        return max(0, min(DEVICE_MAX_VIEWS, n_folders - int(env)))
+    if not layout or not layout[2]:
+        return 0
+    n_cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    return plan_split(n_folders, layout[0], layout[1], threads or FR.decode_threads(), RATES.host_s_per_mb(),
+                      RATES.dev_s_per_mb(), n_cus).n_dev
 
 
 _Z_POOL: list = []
@@ -264,7 +365,9 @@ def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", 
         def one(i):
             p = files[i]
             dst = base + i * stride
+            t = time.perf_counter()
             if L.slg_png_gray8_decode(os.fsencode(p), ctypes.c_void_p(dst), n_px, W, H) == 0:
+                RATES.add_host(time.perf_counter() - t, n_px / 1e6)
                 return
             a = FR.imread_gray(p)                   # any other file: the general decoder
             if a.shape != (H, W):
@@ -333,9 +436,12 @@ def _read_png_general(folder: str, files, need, pool: PinnedPool) -> HostView:
     tbuf = pool.get(n_px * 3) if color else None
     order = list(need) if (0 in need or not color) else [0] + list(need)
 
+    mb = n_px * {0: 1, 2: 3, 3: 1, 4: 2, 6: 4}.get(info0[2], 1) * max(1, info0[3] // 8) / 1e6
+
     def one(i):
         info = (ctypes.c_int32 * 7)()
         tex = i == 0 and tbuf is not None
+        t = time.perf_counter()
         rc = L.slg_png_read(os.fsencode(files[i]), ctypes.c_void_p(base + i * stride), n_px,
                             ctypes.c_void_p(tbuf.data_ptr()) if tex else None, 3 * n_px if tex else 0, info)
         if rc != 0:
@@ -344,6 +450,7 @@ def _read_png_general(folder: str, files, need, pool: PinnedPool) -> HostView:
             raise AttributeError("'NoneType' object has no attribute 'astype'")
         if (info[0], info[1]) != (W, H):
             raise ValueError("all frames must have the same size")
+        RATES.add_host(time.perf_counter() - t, mb)
     try:
         FR.decode_all(one, order)
     except BaseException:
@@ -509,6 +616,8 @@ class PipelineStats:
         self.gpu_ms = 0.0             # GPU: reconstruct launches (stats + fused) of every group
         self.folders_host = 0
         self.folders_device = 0
+        self.probe_s = 0.0            # host: the first folder decoded before the split was planned
+        self.split = None             # the rate model's inputs and decision (plan_split)
         self.wall_s = 0.0
         # SLG_PIPE_TRACE=1: a timeline of (stage, thread, start_s, end_s, what) from the run's
         # start -- host spans from perf_counter, GPU spans from HIP events (tools/e2e_files.py)
@@ -538,7 +647,8 @@ class PipelineStats:
                 "device_kernels_ms": round(self.device_kernels_ms, 3),
                 "device_enqueue_ms": round(self.device_enqueue_s * 1e3, 2),
                 "gpu_reconstruct_ms": round(self.gpu_ms, 3), "folders_host_decoded": self.folders_host,
-                "folders_device_decoded": self.folders_device}
+                "folders_device_decoded": self.folders_device, "probe_ms": round(self.probe_s * 1e3, 2),
+                "split": self.split}
 
 
 LAST_STATS: PipelineStats | None = None     # the stats of the last BatchPipeline.run (tools/e2e_files.py)
@@ -711,8 +821,13 @@ class BatchPipeline:
             self.stats.add("device_decode_ms", g.uploaded[0].elapsed_time(g.uploaded[1]))
             self.stats.gpu_span("gpu_device_decode", *g.uploaded)
             if len(getattr(g, "marks", ())) == 2:         # the inflate + un-filter launches alone
-                self.stats.add("device_kernels_ms", g.marks[0].elapsed_time(g.marks[1]))
+                ms = g.marks[0].elapsed_time(g.marks[1])
+                self.stats.add("device_kernels_ms", ms)
                 self.stats.gpu_span("gpu_inflate", *g.marks)
+                mb = max((hv.width * hv.height * hv.channels / 1e6 for _, hv, _ in g.views if hv.kind == "png_z"),
+                         default=0.0)
+                if mb > 0:
+                    RATES.add_device(ms / 1e3, mb)          # the launch's latency per MB of its largest frame
         from .processing import reconstruct_view
         with torch.cuda.stream(self.format_stream):
             redo = {k for k, _, dev in g.views if png_failed(dev)}
@@ -778,7 +893,29 @@ class BatchPipeline:
         success = 0
         order = [f for f, ok in entries if ok]
         mode = device_png_mode()
-        n_dev = device_share(len(order), mode) if self.device_views is None else max(0, min(int(self.device_views), len(order)))
+        pre = {}                                    # folder -> its read, done before the split
+        if self.device_views is not None:
+            n_dev = max(0, min(int(self.device_views), len(order)))
+        elif mode == "auto" and len(order) > 1 and "SLG_PNG_HOST_AHEAD" not in os.environ:
+            layout = _layout(order[0], self.cfg, self.order)
+            if layout[2] and not RATES.host_measured():
+                # no host rate measured in this process yet: the first folder (read first anyway)
+                # is decoded now and timed, then the split is planned on that rate
+                t = time.perf_counter()
+                fut = Future()
+                try:
+                    fut.set_result(self._read(order[0], False))
+                except Exception as e:  # noqa: BLE001 - the folder's error is reported in order
+                    fut.set_exception(e)
+                pre[order[0]] = fut
+                self.stats.add("probe_s", time.perf_counter() - t)
+            n_dev = device_share(len(order) - len(pre), mode, layout)
+            self.stats.split = {"n_dev": n_dev, "folders": len(order), "frames_per_folder": layout[0],
+                                "mb_per_frame": round(layout[1], 3), "device_ok": layout[2],
+                                "threads": FR.decode_threads(), "host_s_per_mb": round(RATES.host_s_per_mb(), 6),
+                                "dev_s_per_mb": round(RATES.dev_s_per_mb(), 4)}
+        else:
+            n_dev = device_share(len(order), mode)
         if mode == "all" and self.device_views is None:
             n_dev = 0                               # every group is read for the device decoder
         if n_dev:
@@ -804,19 +941,20 @@ class BatchPipeline:
         # own, so they do not queue behind the host decoders' folders (or these behind them)
         zpool = ThreadPoolExecutor(max_workers=4) if n_dev else None
         try:
-            success = self._run_groups(entries, order, mode, n_dev, cut, zpool, timed_write)
+            success = self._run_groups(entries, order, mode, n_dev, cut, zpool, timed_write, pre)
         finally:
             if zpool is not None:
                 zpool.shutdown()
         self.stats.wall_s = time.perf_counter() - t_run
         return success
 
-    def _run_groups(self, entries, order, mode, n_dev, cut, zpool, timed_write) -> int:
-        """The group loop of :meth:`run` (reads, device group, launches, collects, writes)."""
+    def _run_groups(self, entries, order, mode, n_dev, cut, zpool, timed_write, pre=None) -> int:
+        """The group loop of :meth:`run` (reads, device group, launches, collects, writes);
+        ``pre``: folder -> the future of a read already done."""
         success = 0
         dev_first = len(order) - n_dev
         with ThreadPoolExecutor(max_workers=2) as reader, ThreadPoolExecutor(max_workers=self.writers) as writer:
-            futs = {}
+            futs = dict(pre or {})
             all_dev = mode == "all"
             dev_group = None
             if n_dev:                                # the device group's zlib streams first: its
@@ -828,7 +966,8 @@ class BatchPipeline:
             def prefetch(upto):
                 nonlocal nxt
                 while nxt < len(host_order) and nxt < upto:
-                    futs[host_order[nxt]] = reader.submit(self._read, host_order[nxt], all_dev)
+                    if host_order[nxt] not in futs:
+                        futs[host_order[nxt]] = reader.submit(self._read, host_order[nxt], all_dev)
                     nxt += 1
 
             # host groups: consecutive entries holding up to `group` folders with images

@@ -190,3 +190,53 @@ def test_decode_all_waits_for_every_call_before_raising():
         FR.decode_all(work, range(8))
     assert sorted(done) == list(range(1, 8))
     assert FR.decode_pool() is FR.decode_pool()
+
+
+def test_split_rate_model():
+    """The host / device PNG split (pipeline.plan_split) from fed rates: the device takes the
+    last folders only while the host's own share still lasts one device launch; the launch cap
+    is the largest view count whose streams fit a measured-good CU-mask stride (15 C2 views)."""
+    from structured_light_for_3d_model_replication_amd import pipeline as PL
+    c2, c5 = 1920 * 1080 / 1e6, 3840 * 2160 / 1e6
+    host, dev = 2.5e-3, 0.112                      # s/MB per thread on the host, s/MB per launch
+    p = PL.plan_split(36, 44, c2, 16, host, dev, 256)
+    assert p.cap == 15 and p.n_dev == 14           # the round-5 measured optimum (36 folders: 14)
+    assert (36 - p.n_dev) * p.host_s_per_folder >= p.device_s > (36 - p.n_dev - 1) * p.host_s_per_folder
+    assert PL.plan_split(5, 44, c2, 16, host, dev, 256).n_dev == 0      # an 8-rank shard's 4-5 folders
+    assert PL.plan_split(12, 44, c2, 16, host, dev, 256).n_dev == 0
+    assert PL.plan_split(5, 44, c2, 2, host, dev, 256).n_dev == 2       # a 2-CPU rank: the device pays
+    assert PL.plan_split(36, 44, c2, 32, host, dev, 256).n_dev == 0     # 32 CPUs out-decode one launch
+    assert PL.plan_split(80, 44, c2, 16, host, dev, 256).n_dev == 15    # capped (ADVICE r5)
+    assert PL.plan_split(12, 46, c5, 16, host, dev, 256).n_dev == 0     # 4K: a launch takes ~1 s
+    assert PL.plan_split(60, 46, c5, 16, host, dev, 256).n_dev == 14       # 46 streams a view: 14 fit
+    assert PL.plan_split(30, 46, c5, 16, host, dev, 256).n_dev == 30 - 17
+    slow = PL.plan_split(36, 44, c2, 16, 2 * host, dev, 256)             # a slower host: more device views
+    assert slow.n_dev == 15
+    assert PL.plan_split(36, 44, c2, 16, host, dev, 64).cap == 3        # fewer CUs: fewer streams fit
+    assert PL.device_view_cap(44, 256) == 15 and PL.device_view_cap(1, 256) == 16
+
+
+def test_split_uses_measured_rates(monkeypatch):
+    """device_share plans on the process's measured rates (RateMeter), the priors only until a
+    host rate is measured; SLG_PNG_HOST_AHEAD keeps the fixed A/B split."""
+    from structured_light_for_3d_model_replication_amd import pipeline as PL
+    m = PL.RateMeter()
+    assert m.host_s_per_mb() == PL.HOST_S_PER_MB_PRIOR and not m.host_measured()
+    m.add_host(0.05, 10.0)
+    assert m.host_measured() and m.host_s_per_mb() == 0.005
+    m.add_device(0.5, 2.0)
+    assert m.dev_s_per_mb() == 0.25
+    monkeypatch.setenv("SLG_PNG_HOST_AHEAD", "30")
+    assert PL.device_share(36, "auto") == 6
+    monkeypatch.delenv("SLG_PNG_HOST_AHEAD")
+    assert PL.device_share(36, "auto", layout=(44, 2.07, False)) == 0      # not device-decodable
+    assert PL.device_share(36, "off", layout=(44, 2.07, True)) == 0 and PL.device_share(36, "all") == 36
+
+
+def test_decode_threads_follow_the_cgroup_quota(monkeypatch):
+    from structured_light_for_3d_model_replication_amd import frames as FR
+    monkeypatch.delenv("SLG_DECODE_THREADS", raising=False)
+    monkeypatch.setattr(FR, "cpu_quota", lambda: 5)
+    assert FR.decode_threads() == min(5, len(__import__("os").sched_getaffinity(0)))
+    monkeypatch.setattr(FR, "cpu_quota", lambda: None)
+    assert FR.decode_threads() == min(64, len(__import__("os").sched_getaffinity(0)))

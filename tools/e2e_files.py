@@ -33,6 +33,8 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--views", type=int, default=36)
+    ap.add_argument("--geom", default="c2", help="c2 (1920x1080, 11+10 bits, 44 frames) | c5 (3840x2160, "
+                                                 "projector 1920x1080, 11+11 bits, 46 frames)")
     ap.add_argument("--runs", default="host:1,host:4,host:8,auto:4,auto:8,device:16",
                     help="comma list of decoder:group[:NAME=VAL+NAME=VAL] (decoder host | auto | device; "
                          "extra environment for that run, e.g. auto:8:SLG_PNG_RESERVE_EVERY=0)")
@@ -46,7 +48,9 @@ def main():
     from structured_light_for_3d_model_replication_amd import pipeline as PL
     from structured_light_for_3d_model_replication_amd import processing as PR
 
-    rig = synth.default_rig(1920, 1080, 1920, 1080)
+    W, H, nf, kw = ((3840, 2160, 46, dict(n_sets_col=11, n_sets_row=11)) if args.geom == "c5"
+                    else (1920, 1080, 44, dict(n_sets_col=11, n_sets_row=10)))
+    rig = synth.default_rig(W, H, 1920, 1080)
     with tempfile.TemporaryDirectory() as tmp:
         calib = os.path.join(tmp, "calib.mat")
         calibration.save_mat(calib, rig.tables())
@@ -54,13 +58,12 @@ def main():
         t = time.perf_counter()
 
         def make(i):
-            v = synth.render_view(rig, 360.0 * i / args.views, seed=i, n_present=44)
+            v = synth.render_view(rig, 360.0 * i / args.views, seed=i, n_present=nf)
             synth.write_capture(v, os.path.join(root, f"obj_{i:02d}_scan"))
         with ThreadPoolExecutor(8) as ex:
             list(ex.map(make, range(args.views)))
         print(f"[e2e] wrote {args.views} captures in {time.perf_counter() - t:.1f}s", file=sys.stderr, flush=True)
         folders = [f.path for f in os.scandir(root) if f.is_dir()]     # the order batch mode uses
-        kw = dict(n_sets_col=11, n_sets_row=10)
         PR.ProcessingLogic.process_multi_ply(calib, folders[0], "single", log_callback=lambda m: None, **kw)  # warm-up
         runs = [(r.split(":") + [""])[:3] for r in args.runs.split(",") if r]
         res, plys, traces = {}, {}, {}
@@ -92,8 +95,8 @@ def main():
                 print(f"[e2e] rep {rep} {key}: {dt / args.views:.4f} s/view {st}", file=sys.stderr, flush=True)
                 plys[key] = [open(os.path.join(f, os.path.basename(f) + ".ply"), "rb").read() for f in folders]
         first = next(iter(plys.values()))
-        out = {"what": "process_multi_ply batch over C2 PNG folders (end to end), s/view per decoder split",
-               "views": args.views, "runs": res,
+        out = {"what": f"process_multi_ply batch over {args.geom.upper()} PNG folders (end to end), s/view per "
+                       "decoder split", "geom": args.geom, "views": args.views, "runs": res,
                "best": min(((k, min(x["s_per_view"] for x in v)) for k, v in res.items()), key=lambda kv: kv[1]),
                "ply_bytes_equal_all_runs": all(p == first for p in plys.values()),
                "ply_mb_per_view": round(sum(len(b) for b in first) / len(first) / 1e6, 2),
@@ -102,7 +105,7 @@ def main():
 
         if args.parts:                                 # the stages one view at a time, serially
             import torch
-            cfg = PR.E.DecodeConfig(1920, 1080, 11, 10, "otsu")
+            cfg = PR.E.DecodeConfig(1920, 1080, kw["n_sets_col"], kw["n_sets_row"], "otsu")
             cal = calibration.load_mat(calib)
             pool = PL.PinnedPool()
             s = torch.cuda.Stream()
@@ -138,12 +141,8 @@ def main():
 
 
 def _quota():
-    try:
-        sys.path.insert(0, ROOT)
-        import bench
-        return bench.cpu_quota()
-    except Exception:  # noqa: BLE001
-        return None
+    from structured_light_for_3d_model_replication_amd import frames as FR
+    return FR.cpu_quota()
 
 
 if __name__ == "__main__":
