@@ -690,6 +690,8 @@ class BatchPipeline:
 
     def _engine(self, h, w):
         key = (h, w)
+        if key in self.engines and self.engines[key][0].max_views < self._max_views:
+            del self.engines[key]                    # a later batch's device group is larger: rebuild
         if key not in self.engines:
             n = self._max_views
             # made on the compute stream: the default stream shares a hardware queue with the
