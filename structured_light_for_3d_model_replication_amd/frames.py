@@ -62,7 +62,7 @@ def _to_gray(im, path) -> np.ndarray:
 
 
 def _is_png(path) -> bool:
-    return str(path).lower().endswith(".png") and not os.environ.get("SLG_PNG_PIL")
+    return str(path).lower().endswith(".png")
 
 
 def _is_png_gray8(path) -> bool:

@@ -99,9 +99,7 @@ def _decode_rgb(path) -> np.ndarray:
 def device_png_mode() -> str:
     """Which PNG captures the GPU decodes (``slg_png_decode_device``), from SLG_PNG_DEVICE:
     ``"1"`` all of them, ``"0"`` none, unset or ``"auto"`` a share of a batch (the last folders,
-    :func:`device_share`) while host threads decode the rest.  SLG_PNG_PIL forces the host."""
-    if os.environ.get("SLG_PNG_PIL"):
-        return "off"
+    :func:`device_share`) while host threads decode the rest."""
     v = os.environ.get("SLG_PNG_DEVICE", "auto")
     return "all" if v == "1" else "off" if v == "0" else "auto"
 
@@ -315,14 +313,11 @@ def read_view_z(folder: str, files, need, pool: PinnedPool) -> HostView | None:
     def one(k):
         return L.slg_png_zstream(os.fsencode(files[need[k]]), ctypes.c_void_p(base + offs[k]), caps[k], infos[k])
     try:
-        # on a pool of their own by default: queued behind the host decoders' frames on the
-        # shared decode pool, the device group's streams (and so its launch) came later
-        if os.environ.get("SLG_Z_POOL", "own") == "shared":
-            rcs = FR.decode_all(one, range(len(need)))
-        else:
-            futs = [_z_pool().submit(one, k) for k in range(len(need))]
-            wait(futs)
-            rcs = [f.result() for f in futs]
+        # on a pool of their own: queued behind the host decoders' frames on the shared decode
+        # pool, the device group's streams (and so its launch) came later (profiles/r6k)
+        futs = [_z_pool().submit(one, k) for k in range(len(need))]
+        wait(futs)
+        rcs = [f.result() for f in futs]
     except BaseException:
         pool.put(buf)                   # (a file vanished, an executor error): the buffer goes back
         raise
@@ -351,7 +346,7 @@ def read_view(folder: str, cfg: E.DecodeConfig, pool: PinnedPool, order=("bmp", 
             return hv
     L = N.lib()
     w, h = ctypes.c_int32(), ctypes.c_int32()
-    gray8 = (files[0].lower().endswith(".png") and not os.environ.get("SLG_PNG_PIL")
+    gray8 = (files[0].lower().endswith(".png")
              and L.slg_png_gray8_size(os.fsencode(files[0]), ctypes.byref(w), ctypes.byref(h)) == 0)
     workers = min(FR.decode_threads(), len(need))
     if gray8:
@@ -984,9 +979,9 @@ class BatchPipeline:
                 groups.append(cur)
             if dev_group is not None:
                 # the inflate launch is enqueued as soon as the device group's streams are read;
-                # the host decoders start meanwhile (SLG_PIPE_HOST_FIRST folders of them, default
-                # the whole read-ahead: two reader threads at most, so the z reads keep CPUs)
-                prefetch(int(os.environ.get("SLG_PIPE_HOST_FIRST", self.depth)))
+                # the host decoders start meanwhile (the whole read-ahead: two reader threads at
+                # most, so the z reads keep CPUs; holding them back measured slower, r6l)
+                prefetch(self.depth)
                 self._start_device_group(dev_group)
             prefetch(self.depth)
             done_imgs = 0
@@ -1000,7 +995,6 @@ class BatchPipeline:
             # ~10 ms per C2 view, profiles/r5n)
             writing: deque = deque()
             max_writing = max(3 * self.writers, 2 * self.group)
-            early_writes = os.environ.get("SLG_PIPE_EARLY_WRITES", "1") != "0"   # (A/B switch)
 
             def flush(block_until: int):
                 nonlocal success
@@ -1024,7 +1018,7 @@ class BatchPipeline:
 
                     def ready(k, r, g=prev, early=early):
                         early[k] = writer.submit(timed_write, g.entries[k][0], r)
-                    res = self._collect(prev, ready if early_writes else None)
+                    res = self._collect(prev, ready)
                     done_imgs += sum(1 for _, fut in prev.entries if fut is not None)
                     prefetch(done_imgs + self.depth)
                     writing.append((prev, self._submit_writes(prev, res, timed_write, writer, early)))

@@ -443,8 +443,9 @@ def test_png_gray8_fast_path_matches_general_decoder(tmp_path):
 
 
 def test_read_capture_native_png_matches_general_decoder(tmp_path, monkeypatch):
-    """Frame ingest of a capture folder (processing.py:49-60,98-99,124): the native PNG path
-    (texture replicated from frame 0's gray decode) equals the general PIL path exactly."""
+    """Frame ingest of a capture folder (processing.py:49-60,98-99,124): the native gray PNG fast
+    path (texture replicated from frame 0's gray decode) equals the general decoder
+    (slg_png_read, pinned to libpng) exactly."""
     from structured_light_for_3d_model_replication_amd import build, synth, engine as E
     from structured_light_for_3d_model_replication_amd import processing as PR, frames as FR
     build.build_native()
@@ -453,7 +454,8 @@ def test_read_capture_native_png_matches_general_decoder(tmp_path, monkeypatch):
     synth.write_capture(v, str(tmp_path / "cap"))
     cfg = E.DecodeConfig(1920, 1080, 11, 11, "otsu")
     stack, tex = PR.read_capture(str(tmp_path / "cap"), cfg)
-    monkeypatch.setenv("SLG_PNG_PIL", "1")
+    monkeypatch.setattr(FR, "_png_gray8", lambda p: None)        # every frame the general way
+    monkeypatch.setattr(FR, "_is_png_gray8", lambda p: False)
     stack2, tex2 = PR.read_capture(str(tmp_path / "cap"), cfg)
     assert np.array_equal(tex, tex2) and tex.shape == (64, 96, 3) and tex.dtype == np.uint8
     assert all((a is None and b is None) or np.array_equal(a, b) for a, b in zip(stack, stack2))
