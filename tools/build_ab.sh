@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B library builds of the product sources with extra -D flags, into ab_libs/<name>.so
-# (tools/ab.py, tools/solo_prof.py, kbench via SLG_LIB).   bash tools/build_ab.sh <name> [-DFLAG=V ...]
+# (tools/ab.py, tools/ab_bench.sh, kbench via SLG_LIB).   bash tools/build_ab.sh <name> [-DFLAG=V ...]
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; shift
