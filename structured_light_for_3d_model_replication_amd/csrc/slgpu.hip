@@ -32,6 +32,7 @@
 #include <string.h>
 #include <limits.h>
 #include <type_traits>
+#include <utility>
 #include <stdlib.h>
 #include <math.h>
 #include <string>
@@ -526,16 +527,22 @@ __device__ __attribute__((always_inline)) inline float percentile95_from_hist(co
 // ---- Otsu histograms on the i8 matrix cores.  For 64 pixels v_k (k = 16 * lane-group + byte),
 // A[m][k] = 16 * [v_k >> 4 == m] and B[k][n] = 16 * [v_k & 15 == n], so one
 // v_mfma_i32_16x16x64_i8 adds 256 x the count of every value v = 16m + n: no LDS atomics (which
-// retire about one lane per clock).  Each lane splits its 16 pixels into hi / lo nibble planes
-// once and stages them in wave-private LDS; an MFMA step then reads its 64 pixels with four
-// broadcast ds_read_b128 (16 lanes share an address) and builds each operand dword in two VALU
-// ops: ((nib ^ (m ^ 15)) + 1) & 0x10 = 16 - (nib ^ m) masked to bit 4, i.e. 0x10 iff nib == m
-// (no carries between bytes: every byte stays in 1..16).  Lane maps checked by
+// retire about one lane per clock).  The 16 lanes of a row group (lane >> 4) hold the same 16
+// pixels, each against its own m or n = lane & 15.  Operand dwords are built in two VALU ops:
+// ((nib ^ (m ^ 15)) + 1) & 0x10 = 16 - (nib ^ m) masked to bit 4, i.e. 0x10 iff nib == m (no
+// carries between bytes: every byte stays in 1..16).  Lane maps checked by
 // tools/mfma_hist_probe.hip; C/D: col = lane & 15, row = 4 * (lane >> 4) + r.
+//
+// main3's carried count (hist_next_count: other waves' pixels) stages nibble planes in LDS and
+// reads them with broadcast ds_read_b128.  stats_kernel counts each wave's own pixels
+// (hist_chunk_dpp): MFMA step i takes row group g's pixels from lane 16 g + i by a DPP
+// row_newbcast folded into the operand's add, so no LDS at all -- the LDS form read 4 KB per wave
+// and step through the CU's LDS port, four waves per CU, which bounded the count.  The folded
+// add cannot also take the xor, so those operands are step functions, 0x10 iff nib >= m
+// ((nib + 16 - m) & 0x10), the MFMA sums S[m][n] = #{hi >= m, lo >= n}, and the wave's
+// histogram is the 2-D difference S[m][n] - S[m+1][n] - S[m][n+1] + S[m+1][n+1] taken once on
+// the accumulators (hist_from_cumulative).
 typedef int v4i32 __attribute__((ext_vector_type(4)));
-#ifndef SLG_HIST_UNROLL
-#define SLG_HIST_UNROLL 4
-#endif
 constexpr int kHistChunk = 1024;            // pixels per wave and MFMA chunk (16 per lane)
 constexpr int64_t kHistMaxChunks = 8000;    // per wave: 8000 * 1024 * 256 < 2^31 (i32 accumulators)
 
@@ -550,30 +557,59 @@ __device__ inline int onehot16(uint32_t nib, uint32_t repx) {      // bytes: 0x1
   return int(((nib ^ repx) + 0x01010101u) & 0x10101010u);
 }
 
-// One wave adds 1024 pixels (pixel c + 16 * lane + byte: white w[], clip(white - black) d[])
-// into its accumulators.  `stage` = this wave's 4 x 64 uint4 of LDS.
-__device__ inline void mfma_hist_chunk(uint4* stage, const uint32_t (&w)[4], const uint32_t (&d)[4],
-                                       v4i32& acc_w, v4i32& acc_d) {
-  const int lane = threadIdx.x & 63;
+// Step I of a chunk: per byte 0x10 iff the nibble of lane 16 * (lane >> 4) + I >= m, where
+// c = (16 - m) per byte, m = lane & 15.  Bytes stay in 1..31: no carries.
+template <int I>
+__device__ inline int ge16_bcast(uint32_t plane, uint32_t c) {
+  const uint32_t b = uint32_t(__builtin_amdgcn_update_dpp(0, int(plane), 0x150 + I, 0xf, 0xf, false));  // row_newbcast:I
+  return int((b + c) & 0x10101010u);
+}
+
+// pl: the lane's 16 pixels as nibble planes {hi(w)[4], lo(w)[4], hi(d)[4], lo(d)[4]}
+template <int I>
+__device__ inline void hist_step_dpp(const uint32_t (&pl)[16], uint32_t c, v4i32& acc_w, v4i32& acc_d) {
+  const v4i32 aw = {ge16_bcast<I>(pl[0], c), ge16_bcast<I>(pl[1], c), ge16_bcast<I>(pl[2], c), ge16_bcast<I>(pl[3], c)};
+  const v4i32 bw = {ge16_bcast<I>(pl[4], c), ge16_bcast<I>(pl[5], c), ge16_bcast<I>(pl[6], c), ge16_bcast<I>(pl[7], c)};
+  const v4i32 ad = {ge16_bcast<I>(pl[8], c), ge16_bcast<I>(pl[9], c), ge16_bcast<I>(pl[10], c), ge16_bcast<I>(pl[11], c)};
+  const v4i32 bd = {ge16_bcast<I>(pl[12], c), ge16_bcast<I>(pl[13], c), ge16_bcast<I>(pl[14], c), ge16_bcast<I>(pl[15], c)};
+  acc_w = __builtin_amdgcn_mfma_i32_16x16x64_i8(aw, bw, acc_w, 0, 0, 0);
+  acc_d = __builtin_amdgcn_mfma_i32_16x16x64_i8(ad, bd, acc_d, 0, 0, 0);
+}
+
+template <int... Is>
+__device__ inline void hist_steps_dpp(std::integer_sequence<int, Is...>, const uint32_t (&pl)[16], uint32_t c,
+                                      v4i32& acc_w, v4i32& acc_d) {
+  (hist_step_dpp<Is>(pl, c, acc_w, acc_d), ...);
+}
+
+// One wave adds its 1024 pixels (pixel c + 16 * lane + byte: white w[], clip(white - black) d[])
+// into its cumulative accumulators S_w, S_d (256 x #{hi >= m, lo >= n}).
+__device__ inline void hist_chunk_dpp(const uint32_t (&w)[4], const uint32_t (&d)[4], v4i32& acc_w, v4i32& acc_d) {
   const uint32_t m4 = 0x0f0f0f0fu;
-  stage[lane] = make_uint4((w[0] >> 4) & m4, (w[1] >> 4) & m4, (w[2] >> 4) & m4, (w[3] >> 4) & m4);
-  stage[64 + lane] = make_uint4(w[0] & m4, w[1] & m4, w[2] & m4, w[3] & m4);
-  stage[128 + lane] = make_uint4((d[0] >> 4) & m4, (d[1] >> 4) & m4, (d[2] >> 4) & m4, (d[3] >> 4) & m4);
-  stage[192 + lane] = make_uint4(d[0] & m4, d[1] & m4, d[2] & m4, d[3] & m4);
-  // same-wave LDS accesses complete in order: no barrier between these writes and the reads
-  const uint32_t repx = (uint32_t(lane & 15) * 0x01010101u) ^ m4;
-  // (fully unrolled, the scheduler hoisted all 64 LDS reads: 307 VGPRs, one wave per SIMD)
-#pragma unroll SLG_HIST_UNROLL
-  for (int i = 0; i < 16; ++i) {
-    const int src = 4 * i + (lane >> 4);
-    const uint4 hw = stage[src], lw = stage[64 + src], hd = stage[128 + src], ld = stage[192 + src];
-    const v4i32 aw = {onehot16(hw.x, repx), onehot16(hw.y, repx), onehot16(hw.z, repx), onehot16(hw.w, repx)};
-    const v4i32 bw = {onehot16(lw.x, repx), onehot16(lw.y, repx), onehot16(lw.z, repx), onehot16(lw.w, repx)};
-    const v4i32 ad = {onehot16(hd.x, repx), onehot16(hd.y, repx), onehot16(hd.z, repx), onehot16(hd.w, repx)};
-    const v4i32 bd = {onehot16(ld.x, repx), onehot16(ld.y, repx), onehot16(ld.z, repx), onehot16(ld.w, repx)};
-    acc_w = __builtin_amdgcn_mfma_i32_16x16x64_i8(aw, bw, acc_w, 0, 0, 0);
-    acc_d = __builtin_amdgcn_mfma_i32_16x16x64_i8(ad, bd, acc_d, 0, 0, 0);
+  const uint32_t c = (16u - uint32_t(threadIdx.x & 15)) * 0x01010101u;
+  uint32_t pl[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    pl[q] = (w[q] >> 4) & m4; pl[4 + q] = w[q] & m4;
+    pl[8 + q] = (d[q] >> 4) & m4; pl[12 + q] = d[q] & m4;
   }
+  hist_steps_dpp(std::make_integer_sequence<int, 16>(), pl, c, acc_w, acc_d);
+}
+
+// S (this lane's C/D entries: row 4 * (lane >> 4) + r, col lane & 15) -> the histogram entries
+// S[m][n] - S[m+1][n] - S[m][n+1] + S[m+1][n+1], S past row / column 15 being 0.
+__device__ inline v4i32 hist_from_cumulative(v4i32 s) {
+  const int lane = threadIdx.x & 63;
+  const int below = __shfl_down(s[0], 16);        // row 4 * (g + 1): lane + 16, same column
+  v4i32 dm;
+  dm[0] = s[0] - s[1]; dm[1] = s[1] - s[2]; dm[2] = s[2] - s[3]; dm[3] = s[3] - (lane < 48 ? below : 0);
+  v4i32 h;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int right = __shfl_down(dm[r], 1);       // column n + 1: lane + 1
+    h[r] = dm[r] - ((lane & 15) != 15 ? right : 0);
+  }
+  return h;
 }
 
 // 16 pixels of white and clip(white - black) for lane `lane` of the chunk at c; bytes at or
@@ -607,7 +643,6 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
   constexpr int kRow = 257;
   __shared__ __attribute__((aligned(16))) uint32_t sh[16 * 2 * kRow];
   static_assert(512 * 4 + 2 * kOtsuLds * 8 <= 16 * 2 * kRow * 4, "Otsu tail: histograms + two waves' LDS");
-  __shared__ uint4 s_stage[(kBlock / 64) * 256];   // Otsu: per wave hi/lo nibble planes of w, d
   __shared__ uint32_t s_maxd;
   __shared__ uint32_t s_last;
   __shared__ int64_t s_above[2];
@@ -642,7 +677,7 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
 
   // hist kinds: otsu -> [0] white, [1] clip(white-black); percentile -> [0] black.
   const bool otsu = p.thresh_mode == SLG_THRESH_OTSU;
-  if (otsu) {                                  // matrix-core histograms (mfma_hist_chunk)
+  if (otsu) {                                  // matrix-core histograms (hist_chunk_dpp)
     v4i32 acc_w = {0, 0, 0, 0}, acc_d = {0, 0, 0, 0};
     const int lane = tid & 63;
     const int64_t step = int64_t(gridDim.x) * (kBlock / 64) * kHistChunk;
@@ -653,12 +688,14 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
       uint32_t wn[4], dn[4];
       const bool more = c + step < p.n_px;
       if (more) hist_load(white, black, c + step, p.n_px, wn, dn);
-      mfma_hist_chunk(s_stage + wave * 256, w, d, acc_w, acc_d);
+      hist_chunk_dpp(w, d, acc_w, acc_d);
       if (more) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) { w[q] = wn[q]; d[q] = dn[q]; }
       }
     }
+    acc_w = hist_from_cumulative(acc_w);
+    acc_d = hist_from_cumulative(acc_d);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {              // wave sub-histograms: row-major bins 16*row + col
       const int bin = 16 * (4 * (lane >> 4) + r) + (lane & 15);

@@ -74,9 +74,6 @@ def main():
         print(name, r, file=sys.stderr, flush=True)
 
     run("stats", lambda v: eng.stats(dfr[v], cfg))
-    os.environ["SLG_DBG"] = "16"                     # Otsu replaced by a constant: the tail's share
-    run("stats_no_otsu", lambda v: eng.stats(dfr[v], cfg))
-    os.environ.pop("SLG_DBG")
     # one view's whole drop-in call (_gray_decode + _reconstruct_point_cloud fused): stats + main
     # in one event pair, f32 and the drop-in's f64
     for tag, x64 in (("", False), ("_f64", True)):
@@ -100,9 +97,6 @@ def main():
         beng.stats(pb)
         torch.cuda.synchronize()
         run(f"stats_batch{nb}", lambda v: beng.stats(pb))
-        os.environ["SLG_DBG"] = "16"                 # Otsu replaced by a constant
-        run(f"stats_batch{nb}_no_otsu", lambda v: beng.stats(pb))
-        os.environ.pop("SLG_DBG")
         tags = [("", None)]
         if nb == len(dfr):
             dl = os.environ.get("KBENCH_DBG", "1,2,4,3,5,6,7,8,128,11,131")
@@ -225,8 +219,6 @@ def main():
     run("tri_rm1", lambda v: eng.triangulate(maps[v][0], maps[v][1], maps[v][2], dfr[v].texture, dcal, 1,
                                              xyz_f64=False, out=clouds[1]),
         alg_bytes=9 * n_px + 18 * pts[1])
-    os.environ["SLG_DBG"] = "16"
-    run("stats_no_otsu", lambda v: eng.stats(dfr[v], cfg))
     for dbg in (1, 2, 4, 3, 7):        # profiling instance (row_mode 1, f32, frames, pinhole)
         os.environ["SLG_DBG"] = str(dbg)
         run(f"main_rm1_dbg{dbg}", lambda v: eng.decode_triangulate(dfr[v], cfg, dcal, clouds[1], 1),
