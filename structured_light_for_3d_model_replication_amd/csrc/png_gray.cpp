@@ -720,9 +720,8 @@ int libpng_read(const LibPng& L, const std::vector<uint8_t>& file, bool color, u
   return kOk;
 }
 
-const LibPng* g_reader_lib = nullptr;
 void mem_read(void* png, uint8_t* out, size_t n) {
-  MemReader* r = static_cast<MemReader*>(g_reader_lib->get_io_ptr(png));
+  MemReader* r = static_cast<MemReader*>(libpng()->get_io_ptr(png));   // (loaded: libpng_read runs)
   if (r->at + n > r->b->size()) {                        // png_error would longjmp: fill zeros, let
     memset(out, 0, n);                                   // libpng's own CRC / zlib checks fail
     r->at = r->b->size();
@@ -827,7 +826,6 @@ int32_t slg_png_read(const char* path, uint8_t* gray, int64_t gray_cap, uint8_t*
   info[6] = 0;
   const LibPng* L = libpng();
   if (!restated && L) {
-    g_reader_lib = L;
     info[6] = 1;
     if (gray && (rc = libpng_read(*L, b, false, gray, m.w, m.h)) != kOk) return rc;
     if (bgr && (rc = libpng_read(*L, b, true, bgr, m.w, m.h)) != kOk) return rc;
@@ -837,7 +835,6 @@ int32_t slg_png_read(const char* path, uint8_t* gray, int64_t gray_cap, uint8_t*
   gc.init(m, g);                              // (no libpng: the gAMA / sRGB rule alone)
   rc = decode_general(m, gc, gray, bgr);
   if (rc != kOk && L) {                       // a stream libpng may still read (its call)
-    g_reader_lib = L;
     info[6] = 1;
     if (gray && (rc = libpng_read(*L, b, false, gray, m.w, m.h)) != kOk) return rc;
     if (bgr && (rc = libpng_read(*L, b, true, bgr, m.w, m.h)) != kOk) return rc;
