@@ -22,7 +22,8 @@ duration is longer than the period at which they complete.
 across the ranks (strong scaling): every rank decodes its block, the clouds are gathered to rank
 0 through the C-ABI RCCL gatherv (``slg_gather_*``), the timed region includes it.
 ``--config c5job``: BASELINE configs[4], 8 objects x 72 views at 4K resident in HBM, one job per
-step (bench_c5job.py).  ``--config c4|c5``: the larger single-GPU geometries.  For N>1 on the default config each rank
+step (bench_c5job.py).  ``--config c4band``: ONE C4 view split over the ranks by bands of rows,
+one histogram all-reduce per view (bench_c4band.py, strong scaling).  ``--config c4|c5``: the larger single-GPU geometries.  For N>1 on the default config each rank
 runs its own stream of views (weak scaling, no data-path collective); value = all ranks' points /
 max-over-ranks time.
 
@@ -72,6 +73,9 @@ CONFIGS = {
     "c4": dict(cam=(6000, 4000), proj=(3840, 2160), nsets=(12, 12), n_present=None, views=2, copies=6, batch=2,
                text="C4: 6000x4000 view, projector 3840x2160, 12 col + 12 row Gray bits + inverses + "
                     "white/black (50 frames)"),
+    "c4band": dict(cam=(6000, 4000), proj=(3840, 2160), nsets=(12, 12), n_present=None, views=1, copies=1, batch=1,
+                   text="C4 split: ONE 6000x4000 view, projector 3840x2160, 12 col + 12 row Gray bits + inverses + "
+                        "white/black (50 frames), split over the ranks by bands of rows"),
     "c5": dict(cam=(3840, 2160), proj=(1920, 1080), nsets=(11, 11), n_present=None, views=4, copies=6, batch=4,
                text="C5: 3840x2160 view, projector 1920x1080, 11 col + 11 row Gray bits + inverses + "
                     "white/black (46 frames)"),
@@ -80,7 +84,7 @@ CONFIGS = {
                        "+ inverses + white/black (46 frames), all views resident in HBM, one job per step, "
                        "views sharded over the ranks"),
 }
-REF_CALIBRATION_OF = {"c5job": "c5"}     # workloads timed by tools/ref_vs_port.py under another name
+REF_CALIBRATION_OF = {"c5job": "c5", "c4band": "c4"}     # workloads timed by tools/ref_vs_port.py under another name
 
 
 def row_mode_of(wl) -> int:
@@ -434,7 +438,7 @@ def main():
         if getattr(args, k) is None:
             setattr(args, k, wl[k])
     args.result_out = RESULT_OUT         # (bench_c3 imports this file as module "bench")
-    if args.gray_texture and args.config in ("c3", "c5job"):
+    if args.gray_texture and args.config in ("c3", "c5job", "c4band"):
         raise SystemExit("--gray-texture applies to the single-view configs (c2, c4, c5)")
     if args.config == "c3":
         import bench_c3
@@ -442,6 +446,9 @@ def main():
     if args.config == "c5job":
         import bench_c5job
         return bench_c5job.main(args, wl)
+    if args.config == "c4band":
+        import bench_c4band
+        return bench_c4band.main(args, wl)
 
     import numpy as np
     import torch

@@ -180,6 +180,22 @@ int32_t slg_workspace_set_arena(void *workspace, int64_t ws_stride, int32_t n_sl
 int32_t slg_decode_stats(const slg_capture *cap, const slg_decode_params *dp, void *workspace,
                          void *stream);
 
+/* One view split over ranks by bands of rows ("single huge view"; its one exchange
+ * step).  slg_decode_histograms writes the band's mask histograms, summed over the band, to
+ * hist_out (device uint32[513]): Otsu -> [0..255] white, [256..511] clip(white - black, 0, 255)
+ * (processing.py:63-72); percentile -> [0..255] black, [512] = max(white - black) + 256
+ * (sl_system.py:534-540).  The ranks add [0..511] and take the max of [512] (RCCL all-reduce);
+ * slg_thresholds_from_histograms then sets this band's workspace thresholds from the view's
+ * totals (n_pixels = the whole view's, so the thresholds are the unsplit view's, bit for bit) and
+ * arms it for slg_decode_triangulate of the band (n_band_pixels).  Manual thresholds need no
+ * exchange: slg_decode_stats on the band.  Each band's cloud is its rows' points in pixel order,
+ * so rank-ordered concatenation is the view's cloud (row_mode 2: every band's column cloud, then
+ * every band's row cloud). */
+int32_t slg_decode_histograms(const slg_capture *cap, const slg_decode_params *dp, void *workspace,
+                              uint32_t *hist_out, void *stream);
+int32_t slg_thresholds_from_histograms(const uint32_t *hist, int64_t n_pixels, const slg_decode_params *dp,
+                                       void *workspace, int64_t n_band_pixels, void *stream);
+
 /* Gray decode to correspondence maps (after slg_decode_stats on the same workspace). */
 int32_t slg_decode(const slg_capture *cap, const slg_decode_params *dp, void *workspace,
                    int32_t *col_out, int32_t *row_out, uint8_t *mask_out, void *stream);

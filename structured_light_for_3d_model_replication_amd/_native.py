@@ -91,6 +91,8 @@ EXPORTS = {
     "slg_workspace_init": (c_i32, [c_vp, c_i64, c_vp]),
     "slg_workspace_set_arena": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp]),
     "slg_decode_stats": (c_i32, [ctypes.POINTER(Capture), ctypes.POINTER(DecodeParams), c_vp, c_vp]),
+    "slg_decode_histograms": (c_i32, [ctypes.POINTER(Capture), ctypes.POINTER(DecodeParams), c_vp, c_vp, c_vp]),
+    "slg_thresholds_from_histograms": (c_i32, [c_vp, c_i64, ctypes.POINTER(DecodeParams), c_vp, c_i64, c_vp]),
     "slg_decode": (c_i32, [ctypes.POINTER(Capture), ctypes.POINTER(DecodeParams), c_vp,
                            c_vp, c_vp, c_vp, c_vp]),
     "slg_triangulate": (c_i32, [ctypes.POINTER(Maps), ctypes.POINTER(Calib),

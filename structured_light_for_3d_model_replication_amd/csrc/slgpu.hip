@@ -97,9 +97,9 @@ constexpr int kHistCopies = 16;            // partial histograms: blocks spread 
 constexpr int64_t kHistPartOff = 8192;      // uint32 [kHistCopies][2][256] after the header
 constexpr int64_t kHeaderBytes = 65536;
 static_assert(sizeof(WsHeader) <= kHistPartOff, "header");
-static_assert(offsetof(WsHeader, error) == 3084 && offsetof(WsHeader, above) == 3136 &&
+static_assert(offsetof(WsHeader, error) == 3084 && offsetof(WsHeader, totals) == 3120 && offsetof(WsHeader, above) == 3136 &&
               offsetof(WsHeader, arena_off) == 3152,
-              "header offsets the host reads (engine.py: error word, WS_ABOVE_OFF)");
+              "header offsets the host reads (engine.py: error word, WS_TOTALS_OFF, WS_ABOVE_OFF)");
 
 __host__ __device__ inline int64_t n_tiles_of(int64_t n_px) { return (n_px + kTilePx - 1) / kTilePx; }
 __host__ __device__ inline int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
@@ -200,6 +200,7 @@ struct StatsParams {
   const uint32_t* parts[kMaxBatch];   // parts_kernel: per-tile partial histograms of each view
   int64_t n_parts;                    // tiles per view
   int64_t pad_zero;                   // zero pixels counted past n_px (removed from bin 0)
+  uint32_t* hist_out;                 // one view, histograms only (slg_decode_histograms): no thresholds
 };
 
 // a / b correctly rounded from y = RN(1/b) (Markstein): with y correctly rounded and q1
@@ -634,6 +635,44 @@ __device__ inline void hist_load(const uint8_t* white, const uint8_t* black, int
   }
 }
 
+// The mask thresholds of a view from its summed histograms into ws (stats_kernel's last arriver,
+// hist_thresholds_kernel): Otsu of hg[0..255] (white) and hg[256..511] (clip(white - black)) by
+// waves 0 and 1 concurrently, with the bound of the valid pixels (WsHeader::above); or the
+// percentile rule from hg[0..255] (black) and maxd = max(white - black) + 256.  otsu_lds: two
+// waves' kOtsuLds doubles.  Then the resident-job arena reservation (no cursor: nothing).
+__device__ __attribute__((always_inline)) inline void set_thresholds(const uint32_t* hg, uint32_t maxd, int64_t n_px,
+                                                                     bool otsu, WsHeader* ws, double* otsu_lds,
+                                                                     int64_t* s_above) {
+  const int tid = threadIdx.x, wave = tid >> 6;
+  if (otsu) {
+    if (wave < 2) {                            // wave 0: white, wave 1: clip(w-b); concurrently
+      const double thr = otsu_wave(hg + 256 * wave, n_px, otsu_lds + wave * kOtsuLds);
+      const int m = int_threshold(thr, wave == 0 ? 0 : -255);
+      const int64_t above = hist_at_least_wave(hg + 256 * wave, m, n_px);
+      if ((tid & 63) == 0) {
+        if (wave == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
+        ws->above[wave] = above;
+        s_above[wave] = above;
+      }
+    }
+  } else if (tid < 2) {
+    double thr;
+    if (tid == 0) {
+      const float nf = percentile95_from_hist(hg, n_px);
+      thr = double(nf * 1.5f);                           // noise_floor * 1.5 (float32)
+    } else {
+      const float dr = float(int(maxd) - 256);           // np.max(contrast)
+      thr = double(dr * 0.05f);                          // dynamic_range * 0.05 (float32)
+    }
+    const int m = int_threshold(thr, tid == 0 ? 0 : -255);
+    if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
+    ws->above[tid] = n_px;                     // (the percentile histogram is black's: no bound)
+    s_above[tid] = n_px;
+  }
+  __syncthreads();
+  if (tid == 0) arena_reserve(ws, s_above[0], s_above[1]);
+}
+
 #ifndef SLG_STATS_MINB
 #define SLG_STATS_MINB 1     // stats_kernel workgroups per CU its registers are budgeted for
 #endif
@@ -773,35 +812,33 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
   }
   if (tid == 0) s_maxd = __hip_atomic_load(&ws->max_diff_enc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  if (otsu) {
-    if (wave < 2) {                            // wave 0: white, wave 1: clip(w-b); concurrently
-      const double thr = otsu_wave(hg + 256 * wave, p.n_px, reinterpret_cast<double*>(sh + 512) + wave * kOtsuLds);
-      const int m = int_threshold(thr, wave == 0 ? 0 : -255);
-      const int64_t above = hist_at_least_wave(hg + 256 * wave, m, p.n_px);
-      if ((tid & 63) == 0) {
-        if (wave == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
-        ws->above[wave] = above;
-        s_above[wave] = above;
-      }
-    }
-  } else if (tid < 2) {
-    double thr;
-    if (tid == 0) {
-      const float nf = percentile95_from_hist(hg, p.n_px);
-      thr = double(nf * 1.5f);                           // noise_floor * 1.5 (float32)
-    } else {
-      const float dr = float(int(s_maxd) - 256);         // np.max(contrast)
-      thr = double(dr * 0.05f);                          // dynamic_range * 0.05 (float32)
-    }
-    const int m = int_threshold(thr, tid == 0 ? 0 : -255);
-    if (tid == 0) { ws->smin = m; ws->thr_s = thr; } else { ws->cmin = m; ws->thr_c = thr; }
-    ws->above[tid] = p.n_px;                   // (the percentile histogram is black's: no bound)
-    s_above[tid] = p.n_px;
+  if (p.hist_out) {                            // histograms only: a band of a view split over ranks
+    for (int i = tid; i < 512; i += kBlock) p.hist_out[i] = hg[i];
+    if (tid == 0) p.hist_out[512] = s_maxd;
+  } else {
+    set_thresholds(hg, s_maxd, p.n_px, otsu, ws, reinterpret_cast<double*>(sh + 512), s_above);
   }
-  __syncthreads();
-  if (tid == 0) arena_reserve(ws, s_above[0], s_above[1]);
   for (int i = tid; i < kHistCopies * 512; i += kBlock) hist_part[i] = 0;
   if (tid == 0) { ws->max_diff_enc = 0; ws->ticket = 0; }
+}
+
+// Thresholds of a view whose histograms were summed over the bands of rows the ranks hold
+// (slg_thresholds_from_histograms; SURVEY 8(e), the one exchange step of a single-view split):
+// block 0 runs set_thresholds on hist[513] (as slg_decode_histograms wrote it, summed), every
+// block zeroes this band's look-back words for the following fused launch (kernel boundary).
+__global__ __launch_bounds__(kBlock) void hist_thresholds_kernel(const uint32_t* hist, WsHeader* ws, int64_t n_px,
+                                                                 int32_t thresh_mode, int64_t n_state_words) {
+  __shared__ __attribute__((aligned(16))) uint32_t hg[512 + 4 * kOtsuLds];
+  __shared__ int64_t s_above[2];
+  const int tid = threadIdx.x;
+  uint64_t* states = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(ws) + states_off(0));
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + tid; i < n_state_words; i += int64_t(gridDim.x) * kBlock)
+    states[i] = 0;
+  if (blockIdx.x != 0) return;
+  if (tid == 0) ws->tile_counter = 0;
+  for (int i = tid; i < 512; i += kBlock) hg[i] = hist[i];
+  __syncthreads();
+  set_thresholds(hg, hist[512], n_px, thresh_mode == SLG_THRESH_OTSU, ws, reinterpret_cast<double*>(hg + 512), s_above);
 }
 
 // Otsu thresholds from the per-tile partial histograms a fused launch left in each view's
@@ -2231,8 +2268,9 @@ int debug_flags();
 // launch's next-batch pass) instead of from white/black frames.
 int stats_launch_batch(const uint8_t* const* whites, const uint8_t* const* blacks, int n_views, int64_t n_px,
                        const slg_decode_params* dp, char* workspace, int64_t ws_stride, hipStream_t s,
-                       bool from_parts = false) {
+                       bool from_parts = false, uint32_t* hist_out = nullptr) {
   StatsParams sp{};
+  sp.hist_out = hist_out;
   for (int v = 0; v < n_views; ++v) {
     sp.white[v] = whites ? whites[v] : nullptr;
     sp.black[v] = blacks ? blacks[v] : nullptr;
@@ -2957,6 +2995,39 @@ int32_t slg_decode_stats(const slg_capture* cap, const slg_decode_params* dp, vo
   const int64_t n_px = int64_t(cap->height) * cap->width;
   return stats_launch(cap->frames, cap->frames + cap->frame_stride, n_px, dp, workspace,
                       static_cast<hipStream_t>(stream));
+}
+
+int32_t slg_decode_histograms(const slg_capture* cap, const slg_decode_params* dp, void* workspace,
+                              uint32_t* hist_out, void* stream) {
+  int rc = check_capture(cap);
+  if (rc) return rc;
+  if (!dp || !workspace || !hist_out) return fail(SLG_ERR_INVALID, "NULL argument");
+  if (cap->n_frames < 4)
+    return fail(SLG_ERR_NOT_ENOUGH, "Not enough images (got %d, need at least 4).", cap->n_frames);
+  if (dp->thresh_mode != SLG_THRESH_OTSU && dp->thresh_mode != SLG_THRESH_PERCENTILE)
+    return fail(SLG_ERR_INVALID, "histograms serve Otsu / percentile thresholds (manual ones need none)");
+  if (reinterpret_cast<uintptr_t>(hist_out) & 3) return fail(SLG_ERR_INVALID, "hist_out must be 4-byte aligned");
+  const int64_t n_px = int64_t(cap->height) * cap->width;
+  const uint8_t* white = cap->frames;
+  const uint8_t* black = cap->frames + cap->frame_stride;
+  return stats_launch_batch(&white, &black, 1, n_px, dp, static_cast<char*>(workspace), 0,
+                            static_cast<hipStream_t>(stream), false, hist_out);
+}
+
+int32_t slg_thresholds_from_histograms(const uint32_t* hist, int64_t n_pixels, const slg_decode_params* dp,
+                                       void* workspace, int64_t n_band_pixels, void* stream) {
+  if (!hist || !dp || !workspace) return fail(SLG_ERR_INVALID, "NULL argument");
+  if (n_pixels < 1 || n_band_pixels < 1 || n_band_pixels > n_pixels || n_pixels >= (int64_t(1) << 31))
+    return fail(SLG_ERR_INVALID, "need 1 <= n_band_pixels <= n_pixels < 2^31");
+  if (dp->thresh_mode != SLG_THRESH_OTSU && dp->thresh_mode != SLG_THRESH_PERCENTILE)
+    return fail(SLG_ERR_INVALID, "histograms serve Otsu / percentile thresholds (manual ones need none)");
+  if (reinterpret_cast<uintptr_t>(hist) & 3) return fail(SLG_ERR_INVALID, "hist must be 4-byte aligned");
+  const int64_t nsw = n_state_words(n_band_pixels);
+  int64_t grid = (nsw + kBlock - 1) / kBlock;
+  grid = grid < 1 ? 1 : (grid > 64 ? 64 : grid);
+  hipLaunchKernelGGL(hist_thresholds_kernel, dim3(unsigned(grid)), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                     hist, reinterpret_cast<WsHeader*>(workspace), n_pixels, dp->thresh_mode, nsw);
+  return check_launch("hist_thresholds_kernel");
 }
 
 int32_t slg_decode(const slg_capture* cap, const slg_decode_params* dp, void* workspace, int32_t* col_out,

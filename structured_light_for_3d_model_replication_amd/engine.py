@@ -330,6 +330,32 @@ class Reconstructor:
         N.check(N.lib().slg_decode_stats(ctypes.byref(cap), ctypes.byref(dp), _vp(self.workspace),
                                          _stream(stream)))
 
+    def histograms(self, frames: DeviceFrames, cfg: DecodeConfig, out: torch.Tensor | None = None,
+                   stream=None) -> torch.Tensor:
+        """The capture's mask histograms alone (``slg_decode_histograms``): int32 [513] on the
+        device -- Otsu: white [0..255], clip(white - black) [256..511]; percentile: black
+        [0..255], max(white - black) + 256 at [512].  For a view split by rows over ranks
+        (:mod:`bands`): the ranks sum [0..511] and take the max of [512]."""
+        self._check_geometry(frames.height, frames.width)
+        out = torch.zeros(513, dtype=torch.int32, device=self.device) if out is None else out
+        cap, dp = frames.capture(), cfg.struct()
+        N.check(N.lib().slg_decode_histograms(ctypes.byref(cap), ctypes.byref(dp), _vp(self.workspace), _vp(out),
+                                              _stream(stream)))
+        return out
+
+    def thresholds_from_histograms(self, hist: torch.Tensor, n_px_view: int, cfg: DecodeConfig, stream=None):
+        """Mask thresholds from a whole view's histograms (``slg_thresholds_from_histograms``;
+        ``n_px_view``: the view's pixels), and the workspace armed for :meth:`decode_triangulate`
+        of this engine's band."""
+        dp = cfg.struct()
+        N.check(N.lib().slg_thresholds_from_histograms(_vp(hist), int(n_px_view), ctypes.byref(dp),
+                                                       _vp(self.workspace), self.n_px, _stream(stream)))
+
+    def column_points(self) -> int:
+        """Column-cloud points of the last row_mode-2 launch (``WsHeader.totals[0]``; its cloud is
+        the column cloud, then the row cloud).  One host sync."""
+        return int(self.workspace[WS_TOTALS_OFF: WS_TOTALS_OFF + 8].cpu().view(torch.int64).item())
+
     def decode_triangulate(self, frames: DeviceFrames, cfg: DecodeConfig, calib: DeviceCalib,
                            out: "Cloud", row_mode=1, epipolar_tol=2.0, stream=None,
                            _structs=None):
@@ -360,6 +386,7 @@ class Reconstructor:
 
 MAX_VIEWS_PER_LAUNCH = 16     # kMaxViews in csrc/slgpu.hip
 WS_ABOVE_OFF = 3136           # offsetof(WsHeader, above) in csrc/slgpu.hip (static_assert there)
+WS_TOTALS_OFF = 3120          # offsetof(WsHeader, totals)
 
 
 @dataclass
