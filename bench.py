@@ -633,6 +633,12 @@ def main():
                   "oracle_ok": bool(oracle_ok), "xyz_checksum": checksum}
         if not (same and counts_ok and oracle_ok):
             log(f"[rank {rank}] VERIFY FAILED: {verify}")
+    bad = torch.tensor([0.0 if verify is None or (verify["pipelined_equals_plain_bitwise"] and verify["oracle_ok"]
+                                                  and verify["counts_equal_reference_pass"]) else 1.0],
+                       dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+    verify_failed = bool(bad.item())
 
     stats = torch.tensor([dt, float(total_pts), kern_ms, bytes_alg, bytes_dense], dtype=torch.float64, device=dev)
     if world > 1:
@@ -703,7 +709,9 @@ def main():
                                        f"a valid pixel, {out_b} B per point"}}
         out = {
             "metric": METRIC,
-            "value": round(all_pts / dt_max / 1e6, 2),
+            # a run whose clouds failed verification (any rank) measured nothing valid: no value,
+            # non-zero exit (as bench_c5job)
+            "value": None if verify_failed else round(all_pts / dt_max / 1e6, 2),
             "unit": "Mpoints/s",
             "n_gpus": world,
             "steps": K,
@@ -736,6 +744,8 @@ def main():
         print(json.dumps(out), file=RESULT_OUT, flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if verify_failed:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

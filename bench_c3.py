@@ -211,7 +211,8 @@ def main(args, wl):
                   "gathered_equals_all_ranks": bool(sum(gathered) == int(all_pts)),
                   "rank0_counts_match": gathered[: len(counts_local)] == counts_local,
                   "oracle_view0_ok": view_ok}
-        if not (verify["gathered_equals_all_ranks"] and verify["rank0_counts_match"] and view_ok):
+        verify["ok"] = bool(verify["gathered_equals_all_ranks"] and verify["rank0_counts_match"] and view_ok)
+        if not verify["ok"]:
             log(f"VERIFY FAILED: {verify}")
     if rank == 0:
         frame_b = (2 + 2 * (NC + NR)) * H * W
@@ -221,7 +222,7 @@ def main(args, wl):
         achieved = bytes_rank0 / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else None
         out = {
             "metric": bench.METRIC,
-            "value": round(all_pts / (dt / K) / 1e6, 2),
+            "value": None if verify is not None and not verify["ok"] else round(all_pts / (dt / K) / 1e6, 2),
             "unit": "Mpoints/s",
             "n_gpus": world,
             "steps": K,
@@ -260,3 +261,5 @@ def main(args, wl):
         gather.close()
     if world > 1:
         dist.destroy_process_group()
+    if verify is not None and not verify["ok"]:
+        sys.exit(1)

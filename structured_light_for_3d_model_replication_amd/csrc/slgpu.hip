@@ -1892,7 +1892,10 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
   constexpr int NC = KT ? 1 : 3;
   XT pts[NS][kIt][NC];
   uint64_t km[NS][kIt];
-  static_assert(kIt % SLG_TRI_GROUP == 0, "grouped rounds");
+  // full groups, then a pair, then a single round: the tail takes at most 3 rounds, so groups
+  // of 1, 2 or 4 (8 left rounds 4..7 of a tile uncomputed: wrong counts, caught by bench verify)
+  static_assert(kIt % SLG_TRI_GROUP == 0 && (SLG_TRI_GROUP == 1 || SLG_TRI_GROUP == 2 || SLG_TRI_GROUP == 4),
+                "grouped rounds");
   const bool trivial = PROF && (p.dbg & 2);          // ablation: no triangulation arithmetic
   if (p.rays_fast && !trivial) {
     // Several rounds per step: independent straight-line fp64 chains per lane whose plane
