@@ -65,7 +65,8 @@ for step in "$@"; do
       # the raw traces run to tens of MB; gpurun copies back at most 64 MiB per call
       find "$pdir" -name "*.csv" -size +512k -exec gzip -f {} \; ;;
     sq)
-      bash "$R/tools/pmc_main.sh" "$TAG/sq" || { echo "[gpu.sh] SQ FAILED"; exit $n; } ;;
+      bash "$R/tools/pmc_main.sh" "$TAG/sq" || { echo "[gpu.sh] SQ FAILED"; exit $n; }
+      find "$O/sq" -name "*.csv" -size +512k -exec gzip -f {} \; ;;
     ab)
       libs=${rest%,[0-9]*}; rounds=${rest##*,}
       [ "$libs" = "$rest" ] && rounds=4
