@@ -8,6 +8,8 @@
 //   dense8   every lane reads 8 B of every frame             (main3's load width, no mask)
 //   mf8      8 B per frame only in lanes whose mask byte is set (main3's mask-first shape); the
 //            lane decision comes from a 1-byte-per-lane table (its bytes reported separately)
+//   mf16     16 B per frame in lanes of 16 pixels holding a valid one: the same 128-B lines as
+//            mf8 (a lane's 16 bytes never straddle one), half the load instructions
 // Write variants (lane i writes record i, consecutive lanes consecutive records):
 //   st16     16 B per lane (dwordx4, the guide's calibrated shape)
 //   st12     12 B per lane (dwordx3: main3's XYZ stores)
@@ -92,11 +94,15 @@ int main(int argc, char** argv) {
     if (!fp || fread(mask.data(), 1, kNpx, fp) != size_t(kNpx)) { printf("bad mask file\n"); return 1; }
     fclose(fp);
   }
-  std::vector<uint8_t> lv(lanes8, 0), all8(lanes8, 1), all16(lanes16, 1);
-  int64_t valid_lanes = 0, valid_px = 0;
+  std::vector<uint8_t> lv(lanes8, 0), lv16(lanes16, 0), all8(lanes8, 1), all16(lanes16, 1);
+  int64_t valid_lanes = 0, valid_px = 0, valid_lanes16 = 0;
   for (int64_t l = 0; l < lanes8; ++l) {
     for (int k = 0; k < 8; ++k) lv[l] |= mask[8 * l + k] != 0, valid_px += mask[8 * l + k] != 0;
     valid_lanes += lv[l];
+  }
+  for (int64_t l = 0; l < lanes16; ++l) {
+    lv16[l] = lv[2 * l] | lv[2 * l + 1];
+    valid_lanes16 += lv16[l];
   }
   const size_t view = size_t(kNF) * kStride;
   std::vector<uint8_t*> bufs(kNCOPY);
@@ -105,6 +111,8 @@ int main(int argc, char** argv) {
   for (auto& b : bufs) { CK(hipMalloc(&b, view)); CK(hipMemcpy(b, host.data(), view, hipMemcpyHostToDevice)); }
   uint8_t* d_lv; uint32_t* sink;
   CK(hipMalloc(&d_lv, lanes8)); CK(hipMemcpy(d_lv, lv.data(), lanes8, hipMemcpyHostToDevice));
+  uint8_t* d_lv16;
+  CK(hipMalloc(&d_lv16, lanes16)); CK(hipMemcpy(d_lv16, lv16.data(), lanes16, hipMemcpyHostToDevice));
   CK(hipMalloc(&sink, 64));
   const int64_t n_st = 4 << 20;                    // records per store dispatch
   std::vector<uint8_t*> obufs(kNCOPY);
@@ -125,6 +133,7 @@ int main(int argc, char** argv) {
   const double t_d16 = timeit([&](int c) { hipLaunchKernelGGL((rd_kernel<16, 0>), dim3(g16), dim3(kBlock), 0, 0, bufs[c], nullptr, lanes16, sink); });
   const double t_d8 = timeit([&](int c) { hipLaunchKernelGGL((rd_kernel<8, 0>), dim3(g8), dim3(kBlock), 0, 0, bufs[c], nullptr, lanes8, sink); });
   const double t_mf = timeit([&](int c) { hipLaunchKernelGGL((rd_kernel<8, 1>), dim3(g8), dim3(kBlock), 0, 0, bufs[c], d_lv, lanes8, sink); });
+  const double t_mf16 = timeit([&](int c) { hipLaunchKernelGGL((rd_kernel<16, 1>), dim3(g16), dim3(kBlock), 0, 0, bufs[c], d_lv16, lanes16, sink); });
   const unsigned gs = unsigned((n_st + kBlock - 1) / kBlock);
   const double t_s16 = timeit([&](int c) { hipLaunchKernelGGL(st_kernel<16>, dim3(gs), dim3(kBlock), 0, 0, obufs[c], n_st); });
   const double t_s12 = timeit([&](int c) { hipLaunchKernelGGL(st_kernel<12>, dim3(gs), dim3(kBlock), 0, 0, obufs[c], n_st); });
@@ -144,6 +153,9 @@ int main(int argc, char** argv) {
   printf("\"rd_kernel<8, 1>\": {\"what\": \"mf8\", \"requested\": %lld, \"b32\": %lld, \"b64\": %lld, \"b128\": %lld, \"us\": %.2f}, ",
          (long long)req_mf, (long long)blocks_holding(lv, 8, 32) * 32, (long long)blocks_holding(lv, 8, 64) * 64,
          (long long)blocks_holding(lv, 8, 128) * 128, t_mf);
+  printf("\"rd_kernel<16, 1>\": {\"what\": \"mf16\", \"requested\": %lld, \"b32\": %lld, \"b64\": %lld, \"b128\": %lld, \"us\": %.2f}, ",
+         (long long)(int64_t(kNF) * 16 * valid_lanes16), (long long)blocks_holding(lv16, 16, 32) * 32,
+         (long long)blocks_holding(lv16, 16, 64) * 64, (long long)blocks_holding(lv16, 16, 128) * 128, t_mf16);
   printf("\"st_kernel<16>\": {\"what\": \"st16\", \"requested\": %lld, \"us\": %.2f}, ", (long long)(16 * n_st), t_s16);
   printf("\"st_kernel<12>\": {\"what\": \"st12\", \"requested\": %lld, \"us\": %.2f}, ", (long long)(12 * n_st), t_s12);
   printf("\"st_kernel<3>\": {\"what\": \"st3\", \"requested\": %lld, \"us\": %.2f}}}\n", (long long)(3 * n_st), t_s3);
