@@ -1051,6 +1051,35 @@ __device__ inline uint2 ld_frame8(const MainParams& p, int frame, int64_t lp) {
 #endif
 }
 
+// Paired 16-byte frame loads (two-axis decodes): lanes 2j and 2j+1 own pixels [q, q + 16) of the
+// tile (q = the even lane's px0, a multiple of 16).  For a frame pair (a, a + 1) -- white / black,
+// or a pattern / inverse pair -- the even lane reads 16 bytes of frame a and the odd lane 16 bytes
+// of frame a + 1 at q, then the two trade halves (DPP quad_perm [1,0,3,2]), so each holds its own
+// 8 pixels of both frames.  Half the vector-memory instructions of two 8-byte loads per lane and
+// the same 128-byte lines (tools/fetch_probe.hip: C2's mask-gated reads 11.1 vs 12.1-12.4 us;
+// the bench's C2 step 305.5 vs 309.8 us, f64 neutral, profiles/r7l).  Pairing the texture and the
+// carried white / black loads too measured slower (306.2 / 310.6 us).
+// Needs 16-byte aligned frames and stride (else the 8-byte loads run) and both lanes of a pair
+// active at the trade.
+
+struct PairLd {
+  uint32_t v[4];
+};
+__device__ inline PairLd ld_pair16(const MainParams& p, int frame_a, uint32_t voff) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.frames), 0, 0xffffffff, 0x00020000);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, uint32_t(frame_a) * uint32_t(p.stride),
+                                                       SLG_NT_LOADS ? 2 : 0);   // aux 2: nt
+  return {{v[0], v[1], v[2], v[3]}};
+}
+// a = this lane's 8 bytes of frame a, b = of frame a + 1
+__device__ inline void pair_split(const PairLd& L, bool odd, uint2& a, uint2& b) {
+  const uint32_t s0 = odd ? L.v[0] : L.v[2], s1 = odd ? L.v[1] : L.v[3];
+  const uint32_t r0 = uint32_t(__builtin_amdgcn_update_dpp(0, int(s0), 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  const uint32_t r1 = uint32_t(__builtin_amdgcn_update_dpp(0, int(s1), 0xB1, 0xf, 0xf, false));
+  a = odd ? make_uint2(r0, r1) : make_uint2(L.v[0], L.v[1]);
+  b = odd ? make_uint2(L.v[2], L.v[3]) : make_uint2(r0, r1);
+}
+
 // Decode the 8 pixels of one lane: mask bits + column / row codes.  Frame loads of both axes
 // are issued up to kBatch pairs at a time before any is consumed (memory-level parallelism).
 // `tail` (wave-uniform) is set only in the last tile, where map/texture reads need guards;
@@ -1078,8 +1107,17 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
   if (SRC_FRAMES) {
     const int smin = p.ws->smin, cmin = p.ws->cmin;
     const int64_t lp = px0 < p.n_px ? px0 : 0;
-    const uint2 w = ld_frame8(p, 0, lp);
-    const uint2 bl = ld_frame8(p, 1, lp);
+    // paired 16-byte loads (wave-uniform choice): the pair's base pixel, clamped like lp
+    // (column-only decodes -- row_mode 0, C1's 10 pairs -- measured 2-5 % slower paired: there the
+    // lanes a partner drags into the decode cost more than the halved loads save)
+    const bool paired = ROW_MODE != 0 &&
+                        ((reinterpret_cast<uintptr_t>(p.frames) | uint64_t(p.stride)) & 15) == 0;
+    const bool odd = (threadIdx.x & 1) != 0;
+    const int64_t q = px0 & ~int64_t(15);
+    const uint32_t vo = uint32_t(q < p.n_px ? q : 0) + (odd ? uint32_t(p.stride) : 0u);
+    uint2 w, bl;
+    if (paired) pair_split(ld_pair16(p, 0, vo), odd, w, bl);
+    else { w = ld_frame8(p, 0, lp); bl = ld_frame8(p, 1, lp); }
     if constexpr (MF) {
 #pragma unroll
       for (int k = 0; k < kPx; ++k) {
@@ -1089,14 +1127,46 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
         col[k] = 0;
         row[k] = 0;
       }
-      if (valid == 0u) return;
-      pre(w);                                     // (white bytes: a gray capture's texture)
+      // paired: a pair reads its pattern frames if either lane has a valid pixel (both must
+      // take part in the trades); the other lane's codes are never used
+      const uint32_t go = paired ? (valid | uint32_t(__builtin_amdgcn_update_dpp(0, int(valid), 0xB1, 0xf, 0xf, false)))
+                                 : valid;
+      if (go == 0u) return;
+      if (valid != 0u) pre(w);                    // (white bytes: a gray capture's texture)
     }
     PlaneAcc qc = {{0, 0}, {0, 0}}, qr = {{0, 0}, {0, 0}};
     const int np_c = PLAN ? ((PLAN >> 4) & 15) : p.col_pairs;
     const int np_r = ROW_MODE == 0 ? 0 : (PLAN ? (PLAN & 15) : p.row_pairs);
     // compile-time trip count (kMaxBits pairs max), fully unrolled: only forward, wave-uniform
     // branches remain, so the loads of a batch stay in flight together (no vmcnt(0) per load)
+    if (paired) {
+#pragma unroll
+      for (int b0 = 0; b0 < kMaxBits; b0 += kBatch) {
+        PairLd cl[kBatch], rl[kBatch];
+#pragma unroll
+        for (int g = 0; g < kBatch; ++g)
+          if (b0 + g < np_c) cl[g] = ld_pair16(p, p.col_first + 2 * (b0 + g), vo);
+#pragma unroll
+        for (int g = 0; g < kBatch; ++g)
+          if (b0 + g < np_r) rl[g] = ld_pair16(p, p.row_first + 2 * (b0 + g), vo);
+#pragma unroll
+        for (int g = 0; g < kBatch; ++g)
+          if (b0 + g < np_c) {
+            uint2 pv, iv;
+            pair_split(cl[g], odd, pv, iv);
+            if (b0 + g < 8) acc_pair<false>(qc, pv, iv);
+            else acc_pair<true>(qc, pv, iv);
+          }
+#pragma unroll
+        for (int g = 0; g < kBatch; ++g)
+          if (b0 + g < np_r) {
+            uint2 pv, iv;
+            pair_split(rl[g], odd, pv, iv);
+            if (b0 + g < 8) acc_pair<false>(qr, pv, iv);
+            else acc_pair<true>(qr, pv, iv);
+          }
+      }
+    } else {
 #pragma unroll
     for (int b0 = 0; b0 < kMaxBits; b0 += kBatch) {
       uint2 cp[kBatch], ci[kBatch], rp[kBatch], ri[kBatch];
@@ -1124,6 +1194,7 @@ __device__ inline void decode_lane(const MainParams& p, int64_t px0, bool tail, 
           if (b0 + g < 8) acc_pair<false>(qr, rp[g], ri[g]);
           else acc_pair<true>(qr, rp[g], ri[g]);
         }
+    }
     }
     uint32_t ac[4], ar[4];
     acc_codes(qc, np_c, p.col_pre, p.col_post, ac);
