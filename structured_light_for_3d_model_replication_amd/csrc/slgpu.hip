@@ -1058,7 +1058,8 @@ __device__ inline uint2 ld_frame8(const MainParams& p, int frame, int64_t lp) {
 // 8 pixels of both frames.  Half the vector-memory instructions of two 8-byte loads per lane and
 // the same 128-byte lines (tools/fetch_probe.hip: C2's mask-gated reads 11.1 vs 12.1-12.4 us;
 // the bench's C2 step 305.5 vs 309.8 us, f64 neutral, profiles/r7l).  Pairing the texture and the
-// carried white / black loads too measured slower (306.2 / 310.6 us).
+// carried white / black loads too measured slower or neutral (306.2 / 310.6 us; as buffer loads
+// 311.2 vs 310.5, profiles/r7l).  An unaligned caller stack keeps the 8-byte loads (GPU test).
 // Needs 16-byte aligned frames and stride (else the 8-byte loads run) and both lanes of a pair
 // active at the trade.
 

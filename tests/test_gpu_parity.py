@@ -701,3 +701,38 @@ def test_gray_texture_mode_matches_materialised(name, mods):
         outs[k] = [[t.cpu().numpy() for t in c.result()] for c in clouds[k]]
     for (pa, ca), (pg, cg) in zip(outs["s"], outs["g"]):
         assert np.array_equal(pa, pg) and np.array_equal(ca, cg)
+
+
+@pytest.mark.parametrize("misalign", ["stride", "base"])
+def test_unaligned_frame_stack_takes_the_8_byte_loads(misalign, mods):
+    """Two-axis decodes read frame pairs with paired 16-byte loads when the stack is 16-byte
+    aligned (DeviceFrames always is); a caller's stack with an 8-byte stride remainder or an
+    8-byte base offset (what include/slgpu.h allows) takes the 8-byte loads.  Both must give the
+    golden cloud, the maps path too."""
+    E, PR, N = mods
+    import ctypes
+    import torch
+    z = load_case("proc_c2style")
+    cal = load_calibs()["rig"]
+    ref = E.DeviceFrames(list(z["frames"]), z["texture"])
+    F, n = ref.n_frames, ref.n_px
+    stride = (n + 7) // 8 * 8
+    if misalign == "stride" and stride % 16 == 0:
+        stride += 8                                   # an 8-byte remainder either way
+    off = 8 if misalign == "base" else 0
+    buf = torch.zeros(off + max(F, 2) * stride + 64, dtype=torch.uint8, device=ref.data.device)
+    stack = buf[off: off + max(F, 2) * stride].view(max(F, 2), stride)
+    stack[:F, :n].copy_(ref.data[:F, :n])
+    odd = E.DeviceFrames.allocate(F, ref.height, ref.width)
+    odd.data, odd.stride, odd.texture = stack, stride, ref.texture
+    assert (odd.data.data_ptr() % 16 != 0) == (misalign == "base") and (stride % 16 != 0) == (misalign == "stride")
+    dc = E.DeviceCalib(cal, ref.height, ref.width)
+    cfg = _cfg(E, z["params"])
+    eng = E.Reconstructor(ref.height, ref.width)
+    for rm in (1, 2):
+        P, C = eng.reconstruct(odd, cfg, dc, rm, xyz_f64=True).result()
+        want = expected_cloud(z, cal, rm)
+        assert np.array_equal(P.cpu().numpy(), want[0]) and np.array_equal(C.cpu().numpy(), want[1]), rm
+    col, row, mask = eng.decode(odd, cfg)
+    c2, r2, m2 = eng.decode(ref, cfg)
+    assert torch.equal(col, c2) and torch.equal(row, r2) and torch.equal(mask, m2)
