@@ -156,6 +156,11 @@ const char *slg_build_id(void);
  * of a missing instance return SLG_ERR_UNSUPPORTED instead of reaching the HIP runtime, which
  * aborts on them.  Reads the library file only (no HIP call). */
 int32_t slg_kernel_table(char *buf, int64_t cap);
+/* The symbol of the fused kernel instance that the calling thread's last fused launch picked from
+ * that table, into buf (cap bytes, NUL-terminated); "" when the thread has picked none, or its last
+ * pick found no instance.  A test hook: the GPU suite checks that every instance of the table runs and
+ * matches the oracle.  Host only (no HIP call). */
+int32_t slg_last_kernel(char *buf, int64_t cap);
 
 /* Workspace size for images of n_pixels (covers every mode). */
 int64_t slg_workspace_bytes(int64_t n_pixels);

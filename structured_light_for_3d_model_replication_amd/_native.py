@@ -86,6 +86,7 @@ EXPORTS = {
     "slg_version": (c_i32, []),
     "slg_build_id": (ctypes.c_char_p, []),
     "slg_kernel_table": (c_i32, [ctypes.c_char_p, c_i64]),
+    "slg_last_kernel": (c_i32, [ctypes.c_char_p, c_i64]),
     "slg_last_error": (ctypes.c_char_p, []),
     "slg_workspace_bytes": (c_i64, [c_i64]),
     "slg_workspace_init": (c_i32, [c_vp, c_i64, c_vp]),
@@ -194,6 +195,14 @@ def kernel_table() -> dict:
         name, flag = line.split("\t")
         out[name] = flag == "1"
     return out
+
+
+def last_kernel() -> str:
+    """Symbol of the fused kernel instance this thread's last fused launch picked
+    (``slg_last_kernel``; "" when none)."""
+    buf = ctypes.create_string_buffer(512)
+    check(lib().slg_last_kernel(buf, len(buf)))
+    return buf.value.decode()
 
 
 def check(rc: int):

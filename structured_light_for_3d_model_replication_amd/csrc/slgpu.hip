@@ -2591,10 +2591,14 @@ bool device_has(const std::string& name) {
   return std::binary_search(v.begin(), v.end(), name);
 }
 
+// The instance the calling thread's last pick_main returned (slg_last_kernel; NULL: none).
+thread_local const Main3Inst* g_last_main = nullptr;
+
 // The kernel of a (source, row_mode, xyz, rays, plan) launch: the plan's specialised instance
 // if the table has one, else the generic one; the profiling instance when SLG_DBG asks for it.
 // NULL (and *why set) when the table has none or its device code is missing.
 Main3Fn pick_main(int src, int row_mode, int x64, int rays, int plan, const char** why) {
+  g_last_main = nullptr;
   const bool prof = (debug_flags() & kMainDbgBits) != 0;
   const Main3Inst* hit = nullptr;
   for (int pass = 0; pass < 2 && !hit; ++pass) {
@@ -2615,6 +2619,7 @@ Main3Fn pick_main(int src, int row_mode, int x64, int rays, int plan, const char
     *why = "the library's code object lacks this kernel instance (rebuild libslgpu.so)";
     return nullptr;
   }
+  g_last_main = hit;
   return hit->fn;
 }
 
@@ -3046,6 +3051,16 @@ int32_t slg_kernel_table(char* buf, int64_t cap) {
     }
   }
   return missing;
+}
+
+int32_t slg_last_kernel(char* buf, int64_t cap) {
+  if (!buf || cap < 1) return fail(SLG_ERR_INVALID, "buf NULL or cap < 1");
+  buf[0] = 0;
+  if (!g_last_main) return 0;
+  const std::string name = main3_symbol(*g_last_main);
+  if (int64_t(name.size()) >= cap) return fail(SLG_ERR_INVALID, "buf too small for the symbol");
+  memcpy(buf, name.c_str(), name.size() + 1);
+  return 0;
 }
 
 const char* slg_last_error(void) { return g_err; }
