@@ -5,7 +5,8 @@
 plan-specialised ones per pair-count plan (C2 11+10, 1080p 11+11, C4 12+12, C1 10+0; each
 also in a gray-capture form).  The two SLG_DBG profiling instances are left out.  Each case below is a
 small synthetic view (a ragged 320x200 camera: the tail tile's guarded path) whose decode
-parameters select one instance.  ``slg_last_kernel`` names the instance each launch picked, so
+parameters select one instance.  Its row planes are shifted so that row_mode 1 rejects about two
+points in three.  ``slg_last_kernel`` names the instance each launch picked, so
 the test checks which instance produced each cloud.  f64 clouds must equal the oracle
 (``server/processing.py:127-234`` restated) bit for bit; f32 ones must be within XYZ32_RTOL,
 with colours and point order exact.
@@ -77,7 +78,13 @@ def _view(proj, nsets, n_present):
         v = synth.render_view(rig, 20.0, seed=5, n_present=n_present)
         kw = dict(n_cols=proj[0], n_rows=proj[1], n_sets_col=nsets[0], n_sets_row=nsets[1], thresh_mode="otsu")
         maps = O.decode_processing(list(v.frames), **kw)
-        _views[key] = (v, rig.tables(), maps)
+        # The renderer's rig puts every decoded row within the 2 mm epipolar tolerance.  Shifting
+        # two rows in three of the row planes by 3 mm makes row_mode 1 reject points too.
+        cal = rig.tables()
+        rows = cal["wPlaneRow"].copy()
+        rows[3] += 3.0 * (np.arange(rows.shape[1]) % 3 - 1)
+        cal["wPlaneRow"] = rows
+        _views[key] = (v, cal, maps)
     return _views[key]
 
 
@@ -109,6 +116,8 @@ def test_every_fused_instance_matches_oracle(case):
     P, C = (t.cpu().numpy() for t in out.result())
     Po, Co = O.reconstruct_processing(oc, orow, om, tex, cal, row_mode=rm)
     assert len(Po) > 1000 and P.shape == Po.shape, (P.shape, Po.shape)
+    if rm == 1:
+        assert len(Po) < 0.6 * om.sum()                  # the epipolar test rejected points
     assert np.array_equal(C, Co)
     if x64:
         assert np.array_equal(P, Po), f"max |d| {np.abs(P - Po).max()}"
