@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--size", default="1920x1080")
     ap.add_argument("--views", type=int, default=12)
-    ap.add_argument("--only", default="")
+    ap.add_argument("--only", default="")   # names, comma- or plus-separated
     ap.add_argument("--thresh", default="otsu", choices=("otsu", "percentile"))
     args = ap.parse_args()
     import numpy as np
@@ -62,7 +62,7 @@ def main():
         return {"median_us": round(statistics.median(us), 2), "min_us": round(min(us), 2)}
 
     res = {}
-    want = set(args.only.split(",")) if args.only else None
+    want = set(args.only.replace("+", ",").split(",")) if args.only else None   # "+" too: tools/gpu.sh turns commas into spaces
 
     def run(name, fn, pre=None, alg_bytes=None):
         if want and name not in want:
