@@ -2,6 +2,8 @@
 # One-view latency A/B of look-back poll widths (ab_libs/poll{8,16,32}.so, tools/build_ab.sh
 # -DSLG_POLL_WORDS=N): tools/kbench.py --views 1 per library, rounds interleaved, then the
 # bench-shape A/B (tools/ab.py).  Run from the repo root on the GPU box; logs to gpurun_out/$1/.
+# The 16- and 32-word polls measured slower (profiles/r7x, DESIGN.md §4 "One-view calls") and the
+# SLG_POLL_WORDS knob was not committed: the tree polls 8 words.
 set -o pipefail
 O=gpurun_out/$1
 mkdir -p "$O"
