@@ -70,11 +70,12 @@ struct WsHeader {
   uint32_t hist[3][256];   // otsu: 0 white, 1 clip(white-black,0,255); percentile: 0 black
   uint32_t max_diff_enc;   // max(white-black) + 256 (0 = none yet)
   uint32_t ticket;         // stats_kernel arrival counter
-  uint32_t tile_counter;   // next (view, tile) id of a main3 launch (this slice = its view 0)
+  uint32_t lb_ticket;      // main3 tiles that published their column-stream aggregate (lookback_scan)
   uint32_t error;          // bit 0: look-back spin timeout; 1: a look-back helper ran
   int32_t smin;            // mask: white >= smin
   int32_t cmin;            //       (white - black) >= cmin
-  int32_t pad0[2];
+  uint32_t lb_ticket_row;  // the same for the row stream (row_mode 2)
+  int32_t pad0;
   double thr_s;            // float thresholds (for inspection / tests)
   double thr_c;
   int64_t totals[2];       // column / row stream point totals
@@ -697,7 +698,7 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
   // Arm the compaction state of the following main launch (ordered by the kernel boundary).
   for (int64_t i = int64_t(blockIdx.x) * kBlock + tid; i < p.n_state_words; i += int64_t(gridDim.x) * kBlock)
     states[i] = 0;
-  if (blockIdx.x == 0 && tid == 0) ws->tile_counter = 0;
+  if (blockIdx.x == 0 && tid == 0) ws->lb_ticket = ws->lb_ticket_row = 0;
 
   if (p.thresh_mode == SLG_THRESH_MANUAL) {
     if (blockIdx.x == 0 && tid < 2) {
@@ -835,7 +836,7 @@ __global__ __launch_bounds__(kBlock) void hist_thresholds_kernel(const uint32_t*
   for (int64_t i = int64_t(blockIdx.x) * kBlock + tid; i < n_state_words; i += int64_t(gridDim.x) * kBlock)
     states[i] = 0;
   if (blockIdx.x != 0) return;
-  if (tid == 0) ws->tile_counter = 0;
+  if (tid == 0) ws->lb_ticket = ws->lb_ticket_row = 0;
   for (int i = tid; i < 512; i += kBlock) hg[i] = hist[i];
   __syncthreads();
   set_thresholds(hg, hist[512], n_px, thresh_mode == SLG_THRESH_OTSU, ws, reinterpret_cast<double*>(hg + 512), s_above);
@@ -869,7 +870,7 @@ __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint
   if (act) {                                   // main3 workgroup's upper half only syncs)
     for (int64_t i = int64_t(block) * kBlock + tid; i < n_state_words; i += int64_t(n_blocks) * kBlock)
       states[i] = 0;
-    if (block == 0 && tid == 0) ws->tile_counter = 0;
+    if (block == 0 && tid == 0) ws->lb_ticket = ws->lb_ticket_row = 0;
 
     // thread t owns packed word t (bins 2t, 2t+1 of [white 0..255 | clip 256..511])
     const int64_t per = (n_parts + n_blocks - 1) / n_blocks;
@@ -1502,16 +1503,16 @@ __device__ inline void ld_state8_scalar(const uint64_t* p, uint64_t (&v)[8]) {
 // back-off.  Published values never change (0 -> aggregate -> inclusive), so a stale read only
 // delays the walk, never changes the sum.
 template <bool PROF>
-__device__ bool lookback_scalar(const MainParams& p, uint64_t* st, int tile, int agg, uint64_t& excl_out,
-                                int& help_tile, uint32_t& polls, uint32_t& naps) {
+__device__ bool lookback_scalar(const MainParams& p, uint64_t* st, int tile, int agg, bool published,
+                                uint64_t& excl_out, int& help_tile, uint32_t& polls, uint32_t& naps) {
   const int lane = threadIdx.x & 63;
   if (PROF && (p.dbg & 1)) { excl_out = uint64_t(tile) * kTilePx; return true; }   // ablation: no wait
   if (tile == 0) {
-    if (lane == 0) st_state(&st[0], kFlagInc | uint64_t(agg));
+    if (lane == 0 && !published) st_state(&st[0], kFlagInc | uint64_t(agg));
     excl_out = 0;
     return true;
   }
-  if (lane == 0) st_state(&st[tile], kFlagAgg | uint64_t(agg));
+  if (lane == 0 && !published) st_state(&st[tile], kFlagAgg | uint64_t(agg));
   uint64_t excl = 0;
   int j = tile - 1;                          // newest predecessor not summed yet
   unsigned slept = 0, nap = 1;
@@ -1544,6 +1545,77 @@ __device__ bool lookback_scalar(const MainParams& p, uint64_t* st, int tile, int
   }
   if (lane == 0) st_state(&st[tile], kFlagInc | (excl + uint64_t(agg)));
   excl_out = excl;
+  return true;
+}
+
+// Publishes this tile's aggregate (tile 0: its inclusive prefix) and takes a ticket.  The last of
+// the view's tiles to do so finds every tile's word published: it scans them all, 8 consecutive
+// tiles per lane (a segmented scan: an inclusive word restarts the running sum), publishes every
+// tile's inclusive prefix, and returns true with its own exclusive prefix.  The others return
+// false and walk back (lookback_scalar) as before; a walk that is still polling when the scan
+// lands meets an inclusive prefix at its next poll.  A lone view's launch has every tile in
+// flight at once, so without the scan its walks are ~6.7 polls of ~0.8 us each
+// (profiles/r7w).  The values written are the ones the walks compute, so a word only ever
+// goes 0 -> aggregate -> inclusive prefix, whichever writer gets there first.
+constexpr int kScanPer = 8;                // lookback_scan: consecutive tiles per lane
+constexpr int kScanTiles = 2 * 64 * kScanPer;   // lone views up to 1024 tiles (4.2 MP) take the scan
+template <bool PROF>
+__device__ bool lookback_scan(const MainParams& p, uint64_t* st, int tile, int tiles, int agg, uint32_t* ticket,
+                              uint64_t& excl_out) {
+  const int lane = threadIdx.x & 63;
+  if (PROF && (p.dbg & 1)) return false;     // ablation (lookback_scalar): no wait
+  // (no release / acquire fences: on gfx950 an agent-scope one writes back or invalidates the
+  // L2 -- the bench shape took 716 instead of 313 us per step with them.  The words and the
+  // ticket are agent-scope atomics, performed at the L2 that owns the address, and the ticket is
+  // taken after vmcnt(0): the hardware assumption of stats_kernel's ticket)
+  uint32_t t = 0;
+  if (lane == 0) {
+    st_state(&st[tile], (tile == 0 ? kFlagInc : kFlagAgg) | uint64_t(agg));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  t = __builtin_amdgcn_readfirstlane(t);
+  if (t != uint32_t(tiles - 1)) return false;
+  // kScanPer consecutive tiles per lane: their words loaded at once, summed in the lane, then one
+  // wave-wide segmented scan of the lane totals; blocks of 64 * kScanPer tiles in order
+  uint64_t carry = 0, mine = 0;
+  for (int c0 = 0; c0 < tiles; c0 += 64 * kScanPer) {
+    const int i0 = c0 + kScanPer * lane;
+    uint64_t w[kScanPer];
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) w[k] = i0 + k < tiles ? ld_state(&st[i0 + k]) : 0;
+    uint64_t x = 0;                          // the lane's running segmented sum
+    bool f = false;                          // an inclusive word seen in the lane so far
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      const bool inc = (w[k] >> 62) == 2;
+      x = inc ? (w[k] & kValMask) : x + (w[k] & kValMask);
+      f = f || inc;
+    }
+    uint64_t sx = x;                         // inclusive segmented scan of the lane totals
+    bool sf = f;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t xo = __shfl_up(sx, o);
+      const bool fo = __shfl_up(int(sf), o) != 0;
+      if (lane >= o && !sf) { sx += xo; sf = fo; }
+    }
+    uint64_t ex = __shfl_up(sx, 1);          // the lanes before this one (+ carry unless they hold
+    const bool ef = lane > 0 && __shfl_up(int(sf), 1) != 0;   //  an inclusive word)
+    ex = (lane == 0 ? 0 : ex) + (ef ? 0 : carry);
+    x = ex;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      const bool inc = (w[k] >> 62) == 2;
+      x = inc ? (w[k] & kValMask) : x + (w[k] & kValMask);
+      if (i0 + k < tiles && !inc) st_state(&st[i0 + k], kFlagInc | x);
+      if (i0 + k == tile) mine = x;
+    }
+    carry = __shfl(x, 63);
+  }
+  mine = __builtin_amdgcn_readlane(uint32_t(mine), (tile % (64 * kScanPer)) / kScanPer) |
+         (uint64_t(__builtin_amdgcn_readlane(uint32_t(mine >> 32), (tile % (64 * kScanPer)) / kScanPer)) << 32);
+  excl_out = mine - uint64_t(agg);
   return true;
 }
 
@@ -2072,7 +2144,13 @@ __global__ __launch_bounds__(kTileBlock, ROW_MODE == 2 && XYZ64 ? 2 : SLG_M3_WAV
       uint64_t* st = p.states + int64_t(s) * tiles;
       uint64_t excl;
       int ht;
-      while (!lookback_scalar<PROF>(p, st, tile, agg, excl, ht, polls, naps)) {
+      // a lone view's launch: the last tile to publish scans them all (lookback_scan: 1.3 us
+      // off a one-view call; in 16-view launches the walks are hidden and the scan cost 1.3 %;
+      // views of more than kScanTiles tiles span several waves of workgroups, whose staggered
+      // walks end sooner, while the scan of every tile would delay the last one)
+      const bool lone = P.n_views == 1 && tiles <= kScanTiles;
+      if (!(lone && lookback_scan<PROF>(p, st, tile, tiles, agg, s == 0 ? &p.ws->lb_ticket : &p.ws->lb_ticket_row, excl)))
+      while (!lookback_scalar<PROF>(p, st, tile, agg, lone, excl, ht, polls, naps)) {
         // a predecessor has not published for long (it may not be dispatched yet): publish
         // its aggregate for it, computed by this wave, and look back again
         const int hagg = tile_keep_count_wave<ROW_MODE, SRC_FRAMES, RAYS>(p, ht, s);
