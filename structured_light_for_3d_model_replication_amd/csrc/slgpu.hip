@@ -677,6 +677,28 @@ __device__ __attribute__((always_inline)) inline void set_thresholds(const uint3
 #ifndef SLG_STATS_MINB
 #define SLG_STATS_MINB 1     // stats_kernel workgroups per CU its registers are budgeted for
 #endif
+
+// The view's histogram copies summed into hg[0..511] by 256 lanes (lane t: bins t and t + 256),
+// every copy of both bins loaded before any is summed: one round trip (a loop over the two bins
+// took two, 1.6 us of a one-view call's stats launch).  pad: the zero padding past n_px, taken
+// off bins 0 and 256.  Agent-scope atomic loads: see stats_kernel's ticket.
+__device__ __attribute__((always_inline)) inline void sum_hist_copies(const uint32_t* hist_part, int tid, uint32_t pad,
+                                                                     uint32_t* hg) {
+  uint32_t v[2][kHistCopies];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < kHistCopies; ++c)
+      v[r][c] = __hip_atomic_load(hist_part + c * 512 + tid + 256 * r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int c = 0; c < kHistCopies; ++c) acc += v[r][c];
+    hg[tid + 256 * r] = acc - (tid == 0 ? pad : 0u);
+  }
+}
+
 __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsParams p) {
   // 16 sub-histograms per kind (wave x lane&3), rows padded to 257 words so the copies of one
   // bin sit in different banks: a flat background costs at most 16-way same-address adds.
@@ -802,15 +824,7 @@ __global__ __launch_bounds__(kBlock, SLG_STATS_MINB) void stats_kernel(StatsPara
 
   // Last arriver: read the global histograms, compute thresholds, reset for reuse.
   uint32_t* hg = sh;                           // reuse the sub-histograms for the global ones
-  for (int i = tid; i < 2 * 256; i += kBlock)
-  {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int c = 0; c < kHistCopies; ++c)
-      acc += __hip_atomic_load(hist_part + c * 512 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (otsu && (i & 255) == 0) acc -= uint32_t(p.pad_zero);   // zero padding past n_px
-    hg[i] = acc;
-  }
+  sum_hist_copies(hist_part, tid, otsu ? uint32_t(p.pad_zero) : 0u, hg);
   if (tid == 0) s_maxd = __hip_atomic_load(&ws->max_diff_enc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (p.hist_out) {                            // histograms only: a band of a view split over ranks
@@ -897,14 +911,7 @@ __device__ __attribute__((always_inline)) inline void otsu_from_parts(const uint
   }
   __syncthreads();
   if (!*s_last) return;
-  for (int i = tid; act && i < 512; i += kBlock) {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int c = 0; c < kHistCopies; ++c)
-      acc += __hip_atomic_load(hist_part + c * 512 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((i & 255) == 0) acc -= uint32_t(pad_zero);   // zero padding past n_px
-    hg[i] = acc;
-  }
+  if (act) sum_hist_copies(hist_part, tid, uint32_t(pad_zero), hg);
   __syncthreads();
   if (wave < 2) {                              // wave 0: white, wave 1: clip(w-b); concurrently
     const double thr = otsu_wave(hg + 256 * wave, n_px, reinterpret_cast<double*>(hg + 512) + wave * kOtsuLds);
